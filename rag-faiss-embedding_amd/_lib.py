@@ -1,0 +1,84 @@
+"""ctypes binding of libfx_index.so (include/fx_index.h).
+
+The product path has no CPU fallback: if the HIP library is missing or has
+not been built, importing this module raises immediately.  Build it with
+``make -C rag-faiss-embedding_amd/csrc`` (or ``__graft_entry__.build()``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+_HERE = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("FX_INDEX_LIB", _HERE / "libfx_index.so"))
+
+if not LIB_PATH.exists():
+    raise ImportError(
+        f"{LIB_PATH} not found: the MI355X HIP library is required (build it with "
+        f"`make -C {_HERE / 'csrc'}`); there is no CPU fallback")
+
+lib = ctypes.CDLL(str(LIB_PATH))
+
+F32, BF16, F16 = 0, 1, 2
+METRIC_INNER_PRODUCT, METRIC_L2 = 0, 1
+MEM_HOST, MEM_DEVICE = 0, 1
+MAX_K = 32
+
+_vp = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_i = ctypes.c_int
+_pp = ctypes.POINTER(ctypes.c_void_p)
+
+# name -> (restype, argtypes); every symbol declared in include/fx_index.h
+SIGNATURES = {
+    "fx_last_error": (ctypes.c_char_p, []),
+    "fx_device_count": (_i, [ctypes.POINTER(_i)]),
+    "fx_index_create": (_i, [_i, _i, _i, _i, _pp]),
+    "fx_index_free": (None, [_vp]),
+    "fx_index_set_normalize": (_i, [_vp, _i]),
+    "fx_index_set_stream": (_i, [_vp, _vp]),
+    "fx_index_set_id_offset": (_i, [_vp, _i64]),
+    "fx_index_dim": (_i, [_vp, ctypes.POINTER(_i)]),
+    "fx_index_ntotal": (_i, [_vp, ctypes.POINTER(_i64)]),
+    "fx_index_storage_dtype": (_i, [_vp, ctypes.POINTER(_i)]),
+    "fx_index_metric": (_i, [_vp, ctypes.POINTER(_i)]),
+    "fx_index_reserve": (_i, [_vp, _i64]),
+    "fx_index_add": (_i, [_vp, _i64, _vp, _i, _i]),
+    "fx_index_search": (_i, [_vp, _i64, _vp, _i, _i, _i, _vp, _vp, _i]),
+    "fx_index_last_fallbacks": (_i, [_vp, ctypes.POINTER(_i64)]),
+    "fx_index_reset": (_i, [_vp]),
+    "fx_index_reconstruct_n": (_i, [_vp, _i64, _i64, _vp]),
+    "fx_index_write": (_i, [_vp, ctypes.c_char_p]),
+    "fx_index_read": (_i, [ctypes.c_char_p, _i, _i, _pp]),
+    "fx_merge_shards": (_i, [_i, _i, _i64, _i, _vp, _vp, _vp, _vp, _i, _vp]),
+    "fx_synth_fill": (_i, [_vp, _i64, _i64, _i, _i, ctypes.c_uint64, _i, _vp]),
+    "fx_index_profile": (_i, [_vp, _i]),
+    "fx_index_profile_read": (_i, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                   ctypes.POINTER(_i64)]),
+}
+
+for _name, (_res, _args) in SIGNATURES.items():
+    _fn = getattr(lib, _name)
+    _fn.restype = _res
+    _fn.argtypes = _args
+
+
+class FxError(RuntimeError):
+    """A failure reported by the HIP library (faiss raises RuntimeError)."""
+
+
+def last_error() -> str:
+    msg = lib.fx_last_error()
+    return msg.decode("utf-8", "replace") if msg else ""
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        raise FxError(last_error() or f"fx error {rc}")
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    rc = lib.fx_device_count(ctypes.byref(n))
+    return n.value if rc == 0 else 0

@@ -1,0 +1,617 @@
+// fx_index.cpp -- host implementation of the C ABI declared in
+// include/fx_index.h.  Owns HBM (code matrix, row norms, search workspace),
+// sequences the kernels of fx_kernels.hip on one HIP stream per index, and
+// reproduces faiss's IndexFlatL2 API contract (faiss_store.py:29-128,
+// rag_datastore_manager.py:138-218) at the C level.
+#include "../../include/fx_index.h"
+
+#include <float.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "fx_internal.h"
+
+using namespace fx;
+
+namespace {
+
+thread_local std::string g_err;
+
+int set_err(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                             \
+    do {                                                                                          \
+        hipError_t _e = (expr);                                                                   \
+        if (_e != hipSuccess)                                                                     \
+            return set_err(FX_E_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), __FILE__, \
+                           __LINE__);                                                             \
+    } while (0)
+
+// Restores the caller's current device on scope exit (torch keeps its own
+// notion of the current device per thread).
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        ok = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t want) {
+        if (want <= bytes) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        size_t grow = std::max(want, bytes + bytes / 2);
+        hipError_t e = hipMalloc(&p, grow);
+        if (e == hipSuccess) bytes = grow;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+};
+
+inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+}  // namespace
+
+struct FxIndex {
+    int d = 0, dtype = F32, metric = L2, device = 0, normalize = 0;
+    int row_bytes = 0, kdim = 0;
+    int64_t ntotal = 0, cap_rows = 0, id_offset = 0;
+    char* codes = nullptr;
+    float* norms = nullptr;
+    unsigned* max_sq_bits = nullptr;  // device
+    float max_sq = 0.0f;              // host mirror
+    hipStream_t own_stream = nullptr;
+    hipStream_t user_stream = nullptr;
+    // search workspace
+    DevBuf qin, qf32, qop, qeps, cand_d, cand_i, dws, iws, flag, fbc_d, fbc_i, stage;
+    int64_t last_fallbacks = 0;
+    // profiling
+    bool profile = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_scan, ev_merge;
+    std::mutex mu;
+
+    hipStream_t stream() const { return user_stream ? user_stream : own_stream; }
+};
+
+namespace {
+
+int check_dtype(int dt) { return dt == FX_F32 || dt == FX_BF16 || dt == FX_F16; }
+
+hipError_t grow(FxIndex* h, int64_t need_rows) {
+    if (need_rows <= h->cap_rows) return hipSuccess;
+    int64_t cap = round_up(std::max<int64_t>(need_rows, h->cap_rows + h->cap_rows / 2), TILE_R);
+    char* codes = nullptr;
+    float* norms = nullptr;
+    hipError_t e = hipMalloc(&codes, (size_t)cap * h->row_bytes);
+    if (e != hipSuccess) return e;
+    e = hipMalloc(&norms, (size_t)cap * sizeof(float));
+    if (e != hipSuccess) {
+        (void)hipFree(codes);
+        return e;
+    }
+    hipStream_t s = h->stream();
+    // zero-fill: padding rows of the last tile must be finite
+    e = hipMemsetAsync(codes + (size_t)h->ntotal * h->row_bytes, 0, (size_t)(cap - h->ntotal) * h->row_bytes, s);
+    if (e == hipSuccess) e = hipMemsetAsync(norms + h->ntotal, 0, (size_t)(cap - h->ntotal) * sizeof(float), s);
+    if (e == hipSuccess && h->ntotal > 0) {
+        e = hipMemcpyAsync(codes, h->codes, (size_t)h->ntotal * h->row_bytes, hipMemcpyDeviceToDevice, s);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(norms, h->norms, (size_t)h->ntotal * sizeof(float), hipMemcpyDeviceToDevice, s);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) {
+        (void)hipFree(codes);
+        (void)hipFree(norms);
+        return e;
+    }
+    if (h->codes) (void)hipFree(h->codes);
+    if (h->norms) (void)hipFree(h->norms);
+    h->codes = codes;
+    h->norms = norms;
+    h->cap_rows = cap;
+    return hipSuccess;
+}
+
+// choose corpus splits per query tile: enough workgroups to fill 256 CUs
+// several times over (1 workgroup per CU resident: 129 KiB LDS)
+void plan_scan(const FxIndex* h, int64_t nq, ScanParams& p) {
+    p.n_qtiles = (int)((nq + TILE_Q - 1) / TILE_Q);
+    p.n_ctiles = (int)((h->ntotal + TILE_R - 1) / TILE_R);
+    p.qt_per_xcd = p.n_qtiles >= 8 ? (p.n_qtiles + 7) / 8 : 0;
+    const int eff_q = p.qt_per_xcd > 0 ? 8 * p.qt_per_xcd : p.n_qtiles;
+    int splits = (1024 + eff_q - 1) / eff_q;
+    // at least ~4 tiles per split so the per-split warm-up stays amortised
+    splits = std::min(splits, std::max(1, p.n_ctiles / 4));
+    splits = std::max(1, std::min(splits, p.n_ctiles));
+    p.splits = splits;
+}
+
+int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int k, float* D, int64_t* I,
+              int out_mem) {
+    hipStream_t s = h->stream();
+    const int64_t nq_pad = round_up(nq, TILE_Q);
+    const int qes = dtype_size(q_dtype);
+    // queries -> device
+    const void* qdev = q;
+    if (q_mem == FX_MEM_HOST) {
+        HIP_TRY(h->qin.ensure((size_t)nq * h->d * qes));
+        HIP_TRY(hipMemcpyAsync(h->qin.p, q, (size_t)nq * h->d * qes, hipMemcpyHostToDevice, s));
+        qdev = h->qin.p;
+    }
+    HIP_TRY(h->qf32.ensure((size_t)nq_pad * h->kdim * 4));
+    void* qop = nullptr;
+    if (h->dtype != F32) {
+        HIP_TRY(h->qop.ensure((size_t)nq_pad * h->row_bytes));
+        qop = h->qop.p;
+    }
+    HIP_TRY(h->qeps.ensure((size_t)nq * 4));
+    HIP_TRY(launch_prep_queries(qdev, q_dtype, nq, nq_pad, h->d, h->kdim, h->dtype, h->metric, (float*)h->qf32.p,
+                                qop, (float*)h->qeps.p, sqrt((double)h->max_sq), s));
+
+    ScanParams sp;
+    plan_scan(h, nq, sp);
+    sp.codes = h->codes;
+    sp.norms = h->norms;
+    sp.ntotal = h->ntotal;
+    sp.row_bytes = h->row_bytes;
+    sp.qop = qop ? (const char*)qop : (const char*)h->qf32.p;
+    sp.nq = nq;
+    const size_t ncand = (size_t)sp.n_qtiles * sp.splits * TILE_Q * KP;
+    HIP_TRY(h->cand_d.ensure(ncand * 4));
+    HIP_TRY(h->cand_i.ensure(ncand * 4));
+    sp.cand_d = (float*)h->cand_d.p;
+    sp.cand_i = (int*)h->cand_i.p;
+
+    hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
+    if (h->profile) {
+        HIP_TRY(hipEventCreate(&e0));
+        HIP_TRY(hipEventCreate(&e1));
+        HIP_TRY(hipEventCreate(&e2));
+        HIP_TRY(hipEventRecord(e0, s));
+    }
+    HIP_TRY(launch_scan(h->dtype, h->metric, sp, s));
+    if (h->profile) HIP_TRY(hipEventRecord(e1, s));
+
+    float* Dd = D;
+    int64_t* Id = I;
+    if (out_mem == FX_MEM_HOST) {
+        HIP_TRY(h->dws.ensure((size_t)nq * k * 4));
+        HIP_TRY(h->iws.ensure((size_t)nq * k * 8));
+        Dd = (float*)h->dws.p;
+        Id = (int64_t*)h->iws.p;
+    }
+    HIP_TRY(h->flag.ensure((size_t)(nq + 1) * 4));
+    int* n_flag = (int*)h->flag.p;
+    HIP_TRY(hipMemsetAsync(n_flag, 0, 4, s));
+
+    RefineParams rp;
+    rp.cand_d = sp.cand_d;
+    rp.cand_i = sp.cand_i;
+    rp.splits = sp.splits;
+    rp.nq = nq;
+    rp.k = k;
+    rp.codes = h->codes;
+    rp.row_bytes = h->row_bytes;
+    rp.kdim = h->kdim;
+    rp.qf32 = (const float*)h->qf32.p;
+    rp.qeps = (const float*)h->qeps.p;
+    rp.id_offset = h->id_offset;
+    rp.D = Dd;
+    rp.I = Id;
+    rp.n_flag = n_flag;
+    rp.flag_list = n_flag + 1;
+    HIP_TRY(launch_refine(h->dtype, h->metric, rp, s));
+    if (h->profile) {
+        HIP_TRY(hipEventRecord(e2, s));
+        h->ev_scan.emplace_back(e0, e1);
+        h->ev_merge.emplace_back(e1, e2);
+    }
+
+    // Certification result: uncertified queries are re-ranked by the exact
+    // fp64 scan (rare: only when the candidate margin is inside the scan's
+    // worst-case rounding bound).
+    int nf = 0;
+    HIP_TRY(hipMemcpyAsync(&nf, n_flag, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    h->last_fallbacks = nf;
+    if (nf > 0) {
+        const int fb_splits = (int)std::max<int64_t>(1, std::min<int64_t>(256, (h->ntotal + 4095) / 4096));
+        const int chunk = 64;
+        for (int f0 = 0; f0 < nf; f0 += chunk) {
+            const int nl = std::min(chunk, nf - f0);
+            const size_t per = (size_t)nl * fb_splits * 4 * KP;
+            HIP_TRY(h->fbc_d.ensure(per * 4));
+            HIP_TRY(h->fbc_i.ensure(per * 4));
+            HIP_TRY(launch_exact_fallback(h->dtype, h->metric, h->codes, h->row_bytes, h->kdim, h->ntotal,
+                                          (const float*)h->qf32.p, n_flag + 1 + f0, nl, k, h->id_offset,
+                                          (float*)h->fbc_d.p, (int*)h->fbc_i.p, fb_splits, Dd, Id, s));
+        }
+    }
+    if (out_mem == FX_MEM_HOST) {
+        HIP_TRY(hipMemcpyAsync(D, Dd, (size_t)nq * k * 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(I, Id, (size_t)nq * k * 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    return FX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* fx_last_error(void) { return g_err.c_str(); }
+
+int fx_device_count(int* out) {
+    if (!out) return set_err(FX_E_ARG, "null out");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) {
+        *out = 0;
+        return set_err(FX_E_HIP, "hipGetDeviceCount: %s", hipGetErrorString(e));
+    }
+    *out = n;
+    return FX_OK;
+}
+
+int fx_index_create(int d, int storage_dtype, int metric, int device, FxIndex** out) {
+    if (!out) return set_err(FX_E_ARG, "null out");
+    *out = nullptr;
+    if (d <= 0) return set_err(FX_E_ARG, "dimension must be positive (got %d)", d);
+    if (!check_dtype(storage_dtype)) return set_err(FX_E_ARG, "bad storage dtype %d", storage_dtype);
+    if (metric != FX_METRIC_L2 && metric != FX_METRIC_INNER_PRODUCT)
+        return set_err(FX_E_ARG, "bad metric %d", metric);
+    int n = 0;
+    HIP_TRY(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n) return set_err(FX_E_HIP, "device %d not available (%d devices)", device, n);
+    DeviceGuard g(device);
+    if (!g.ok) return set_err(FX_E_HIP, "hipSetDevice(%d) failed", device);
+    FxIndex* h = new FxIndex();
+    h->d = d;
+    h->dtype = storage_dtype;
+    h->metric = metric;
+    h->device = device;
+    h->row_bytes = (int)round_up((int64_t)d * dtype_size(storage_dtype), ROW_ALIGN);
+    h->kdim = h->row_bytes / dtype_size(storage_dtype);
+    hipError_t e = hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&h->max_sq_bits, 16);
+    if (e == hipSuccess) e = hipMemset(h->max_sq_bits, 0, 16);
+    if (e != hipSuccess) {
+        fx_index_free(h);
+        return set_err(FX_E_HIP, "index init: %s", hipGetErrorString(e));
+    }
+    *out = h;
+    return FX_OK;
+}
+
+void fx_index_free(FxIndex* h) {
+    if (!h) return;
+    {
+        DeviceGuard g(h->device);
+        if (h->own_stream) (void)hipStreamSynchronize(h->own_stream);
+        if (h->user_stream) (void)hipStreamSynchronize(h->user_stream);
+        if (h->codes) (void)hipFree(h->codes);
+        if (h->norms) (void)hipFree(h->norms);
+        if (h->max_sq_bits) (void)hipFree(h->max_sq_bits);
+        for (DevBuf* b : {&h->qin, &h->qf32, &h->qop, &h->qeps, &h->cand_d, &h->cand_i, &h->dws, &h->iws, &h->flag,
+                          &h->fbc_d, &h->fbc_i, &h->stage})
+            b->release();
+        for (auto& pr : h->ev_scan) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
+        for (auto& pr : h->ev_merge) (void)hipEventDestroy(pr.second);
+        if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
+    }
+    delete h;
+}
+
+int fx_index_set_normalize(FxIndex* h, int on) {
+    if (!h) return set_err(FX_E_ARG, "null index");
+    std::lock_guard<std::mutex> lk(h->mu);
+    h->normalize = on ? 1 : 0;
+    return FX_OK;
+}
+
+int fx_index_set_stream(FxIndex* h, void* stream) {
+    if (!h) return set_err(FX_E_ARG, "null index");
+    std::lock_guard<std::mutex> lk(h->mu);
+    h->user_stream = (hipStream_t)stream;
+    return FX_OK;
+}
+
+int fx_index_set_id_offset(FxIndex* h, int64_t off) {
+    if (!h || off < 0) return set_err(FX_E_ARG, "bad index/offset");
+    std::lock_guard<std::mutex> lk(h->mu);
+    h->id_offset = off;
+    return FX_OK;
+}
+
+int fx_index_dim(const FxIndex* h, int* out) {
+    if (!h || !out) return set_err(FX_E_ARG, "null argument");
+    *out = h->d;
+    return FX_OK;
+}
+int fx_index_ntotal(const FxIndex* h, int64_t* out) {
+    if (!h || !out) return set_err(FX_E_ARG, "null argument");
+    *out = h->ntotal;
+    return FX_OK;
+}
+int fx_index_storage_dtype(const FxIndex* h, int* out) {
+    if (!h || !out) return set_err(FX_E_ARG, "null argument");
+    *out = h->dtype;
+    return FX_OK;
+}
+int fx_index_metric(const FxIndex* h, int* out) {
+    if (!h || !out) return set_err(FX_E_ARG, "null argument");
+    *out = h->metric;
+    return FX_OK;
+}
+
+int fx_index_reserve(FxIndex* h, int64_t n) {
+    if (!h || n < 0) return set_err(FX_E_ARG, "bad reserve");
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard g(h->device);
+    HIP_TRY(grow(h, n));
+    return FX_OK;
+}
+
+int fx_index_add(FxIndex* h, int64_t n, const void* x, int x_dtype, int x_mem) {
+    if (!h) return set_err(FX_E_ARG, "null index");
+    if (n < 0) return set_err(FX_E_ARG, "negative n");
+    if (n == 0) return FX_OK;
+    if (!x) return set_err(FX_E_ARG, "null x");
+    if (!check_dtype(x_dtype)) return set_err(FX_E_ARG, "bad x dtype %d", x_dtype);
+    if ((int64_t)h->ntotal + n >= (int64_t)INT32_MAX) return set_err(FX_E_UNSUPPORTED, "more than 2^31-1 rows per shard");
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard g(h->device);
+    hipStream_t s = h->stream();
+    HIP_TRY(grow(h, h->ntotal + n));
+    const size_t xes = dtype_size(x_dtype);
+    if (x_mem == FX_MEM_DEVICE) {
+        HIP_TRY(launch_convert_rows(x, x_dtype, n, h->d, h->codes + (size_t)h->ntotal * h->row_bytes, h->dtype,
+                                    h->kdim, h->norms + h->ntotal, h->max_sq_bits, h->normalize, s));
+    } else {
+        // stream host rows through a bounded staging buffer (<= 256 MiB)
+        const int64_t chunk = std::max<int64_t>(1, (256ll << 20) / ((int64_t)h->d * xes));
+        for (int64_t r0 = 0; r0 < n; r0 += chunk) {
+            const int64_t nr = std::min(chunk, n - r0);
+            HIP_TRY(h->stage.ensure((size_t)nr * h->d * xes));
+            HIP_TRY(hipMemcpyAsync(h->stage.p, (const char*)x + (size_t)r0 * h->d * xes, (size_t)nr * h->d * xes,
+                                   hipMemcpyHostToDevice, s));
+            HIP_TRY(launch_convert_rows(h->stage.p, x_dtype, nr, h->d,
+                                        h->codes + (size_t)(h->ntotal + r0) * h->row_bytes, h->dtype, h->kdim,
+                                        h->norms + h->ntotal + r0, h->max_sq_bits, h->normalize, s));
+            HIP_TRY(hipStreamSynchronize(s));  // staging buffer reuse
+        }
+    }
+    unsigned bits = 0;
+    HIP_TRY(hipMemcpyAsync(&bits, h->max_sq_bits, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    memcpy(&h->max_sq, &bits, 4);
+    h->ntotal += n;
+    return FX_OK;
+}
+
+int fx_index_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int k, float* D, int64_t* I,
+                    int out_mem) {
+    if (!h) return set_err(FX_E_ARG, "null index");
+    if (nq < 0) return set_err(FX_E_ARG, "negative nq");
+    if (k <= 0) return set_err(FX_E_ARG, "k must be positive (got %d)", k);
+    if (k > FX_MAX_K) return set_err(FX_E_UNSUPPORTED, "k=%d exceeds FX_MAX_K=%d", k, FX_MAX_K);
+    if (!check_dtype(q_dtype)) return set_err(FX_E_ARG, "bad query dtype %d", q_dtype);
+    if (nq == 0) return FX_OK;
+    if (!q || !D || !I) return set_err(FX_E_ARG, "null buffer");
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard g(h->device);
+    if (h->ntotal == 0) {
+        // faiss: empty index -> every slot missing (I = -1, D = FLT_MAX)
+        std::vector<float> dv((size_t)nq * k, h->metric == L2 ? FLT_MAX : -FLT_MAX);
+        std::vector<int64_t> iv((size_t)nq * k, -1);
+        if (out_mem == FX_MEM_HOST) {
+            memcpy(D, dv.data(), dv.size() * 4);
+            memcpy(I, iv.data(), iv.size() * 8);
+        } else {
+            HIP_TRY(hipMemcpyAsync(D, dv.data(), dv.size() * 4, hipMemcpyHostToDevice, h->stream()));
+            HIP_TRY(hipMemcpyAsync(I, iv.data(), iv.size() * 8, hipMemcpyHostToDevice, h->stream()));
+            HIP_TRY(hipStreamSynchronize(h->stream()));
+        }
+        h->last_fallbacks = 0;
+        return FX_OK;
+    }
+    return do_search(h, nq, q, q_dtype, q_mem, k, D, I, out_mem);
+}
+
+int fx_index_last_fallbacks(FxIndex* h, int64_t* out) {
+    if (!h || !out) return set_err(FX_E_ARG, "null argument");
+    *out = h->last_fallbacks;
+    return FX_OK;
+}
+
+int fx_index_reset(FxIndex* h) {
+    if (!h) return set_err(FX_E_ARG, "null index");
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard g(h->device);
+    HIP_TRY(hipStreamSynchronize(h->stream()));
+    HIP_TRY(hipMemset(h->max_sq_bits, 0, 4));
+    if (h->codes && h->cap_rows > 0) {
+        HIP_TRY(hipMemset(h->codes, 0, (size_t)h->cap_rows * h->row_bytes));
+        HIP_TRY(hipMemset(h->norms, 0, (size_t)h->cap_rows * sizeof(float)));
+    }
+    h->max_sq = 0.0f;
+    h->ntotal = 0;
+    return FX_OK;
+}
+
+int fx_index_reconstruct_n(FxIndex* h, int64_t i0, int64_t n, float* out) {
+    if (!h || !out || i0 < 0 || n < 0 || i0 + n > h->ntotal) return set_err(FX_E_ARG, "bad reconstruct range");
+    if (n == 0) return FX_OK;
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard g(h->device);
+    hipStream_t s = h->stream();
+    const int64_t chunk = std::max<int64_t>(1, (128ll << 20) / ((int64_t)h->d * 4));
+    for (int64_t r0 = 0; r0 < n; r0 += chunk) {
+        const int64_t nr = std::min(chunk, n - r0);
+        HIP_TRY(h->stage.ensure((size_t)nr * h->d * 4));
+        HIP_TRY(launch_to_f32(h->codes + (size_t)(i0 + r0) * h->row_bytes, h->dtype, h->row_bytes, nr, h->d,
+                              (float*)h->stage.p, s));
+        HIP_TRY(hipMemcpyAsync(out + (size_t)r0 * h->d, h->stage.p, (size_t)nr * h->d * 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    return FX_OK;
+}
+
+int fx_index_write(FxIndex* h, const char* path) {
+    if (!h || !path) return set_err(FX_E_ARG, "null argument");
+    if (h->metric != FX_METRIC_L2) return set_err(FX_E_UNSUPPORTED, "IxF2 writer supports METRIC_L2 only");
+    FILE* f = fopen(path, "wb");
+    if (!f) return set_err(FX_E_IO, "cannot open %s for writing", path);
+    const int32_t d = h->d, metric = FX_METRIC_L2;
+    const int64_t nt = h->ntotal, dummy = 1 << 20, count = h->ntotal * (int64_t)h->d;
+    const uint8_t trained = 1;
+    bool ok = fwrite("IxF2", 1, 4, f) == 4 && fwrite(&d, 4, 1, f) == 1 && fwrite(&nt, 8, 1, f) == 1 &&
+              fwrite(&dummy, 8, 1, f) == 1 && fwrite(&dummy, 8, 1, f) == 1 && fwrite(&trained, 1, 1, f) == 1 &&
+              fwrite(&metric, 4, 1, f) == 1 && fwrite(&count, 8, 1, f) == 1;
+    const int64_t chunk = std::max<int64_t>(1, (64ll << 20) / ((int64_t)h->d * 4));
+    std::vector<float> buf;
+    for (int64_t r0 = 0; ok && r0 < nt; r0 += chunk) {
+        const int64_t nr = std::min(chunk, nt - r0);
+        buf.resize((size_t)nr * h->d);
+        int rc = fx_index_reconstruct_n(h, r0, nr, buf.data());
+        if (rc != FX_OK) {
+            fclose(f);
+            return rc;
+        }
+        ok = fwrite(buf.data(), 4, buf.size(), f) == buf.size();
+    }
+    if (fclose(f) != 0) ok = false;
+    if (!ok) return set_err(FX_E_IO, "short write to %s", path);
+    return FX_OK;
+}
+
+int fx_index_read(const char* path, int storage_dtype, int device, FxIndex** out) {
+    if (!path || !out) return set_err(FX_E_ARG, "null argument");
+    *out = nullptr;
+    FILE* f = fopen(path, "rb");
+    if (!f) return set_err(FX_E_IO, "could not open %s for reading", path);
+    char fourcc[4];
+    int32_t d = 0, metric = 0;
+    int64_t nt = 0, d1 = 0, d2 = 0, count = 0;
+    uint8_t trained = 0;
+    bool ok = fread(fourcc, 1, 4, f) == 4 && fread(&d, 4, 1, f) == 1 && fread(&nt, 8, 1, f) == 1 &&
+              fread(&d1, 8, 1, f) == 1 && fread(&d2, 8, 1, f) == 1 && fread(&trained, 1, 1, f) == 1 &&
+              fread(&metric, 4, 1, f) == 1 && fread(&count, 8, 1, f) == 1;
+    if (!ok) {
+        fclose(f);
+        return set_err(FX_E_IO, "%s: truncated IxF2 header", path);
+    }
+    if (memcmp(fourcc, "IxF2", 4) != 0) {
+        fclose(f);
+        return set_err(FX_E_IO, "%s: unsupported index fourcc (only IxF2 / IndexFlatL2)", path);
+    }
+    if (d <= 0 || nt < 0 || metric != FX_METRIC_L2 || count != nt * (int64_t)d) {
+        fclose(f);
+        return set_err(FX_E_IO, "%s: inconsistent IxF2 header", path);
+    }
+    FxIndex* h = nullptr;
+    int rc = fx_index_create(d, storage_dtype, FX_METRIC_L2, device, &h);
+    if (rc != FX_OK) {
+        fclose(f);
+        return rc;
+    }
+    rc = fx_index_reserve(h, nt);
+    const int64_t chunk = std::max<int64_t>(1, (64ll << 20) / ((int64_t)d * 4));
+    std::vector<float> buf;
+    for (int64_t r0 = 0; rc == FX_OK && r0 < nt; r0 += chunk) {
+        const int64_t nr = std::min(chunk, nt - r0);
+        buf.resize((size_t)nr * d);
+        if (fread(buf.data(), 4, buf.size(), f) != buf.size()) {
+            rc = set_err(FX_E_IO, "%s: truncated IxF2 codes", path);
+            break;
+        }
+        rc = fx_index_add(h, nr, buf.data(), FX_F32, FX_MEM_HOST);
+    }
+    fclose(f);
+    if (rc != FX_OK) {
+        fx_index_free(h);
+        return rc;
+    }
+    *out = h;
+    return FX_OK;
+}
+
+int fx_merge_shards(int metric, int nshards, int64_t nq, int k, const float* D_in, const int64_t* I_in, float* D_out,
+                    int64_t* I_out, int device, void* stream) {
+    if (nshards <= 0 || nq < 0 || k <= 0 || k > 64) return set_err(FX_E_ARG, "bad merge shape");
+    if (!D_in || !I_in || !D_out || !I_out) return set_err(FX_E_ARG, "null buffer");
+    if (metric != FX_METRIC_L2 && metric != FX_METRIC_INNER_PRODUCT) return set_err(FX_E_ARG, "bad metric");
+    DeviceGuard g(device);
+    if (!g.ok) return set_err(FX_E_HIP, "hipSetDevice(%d) failed", device);
+    HIP_TRY(launch_merge_shards(metric, nshards, nq, k, D_in, I_in, D_out, I_out, (hipStream_t)stream));
+    return FX_OK;
+}
+
+int fx_synth_fill(void* out, int64_t row0, int64_t n, int d, int dtype, uint64_t seed, int device, void* stream) {
+    if (!out || n < 0 || d <= 0 || row0 < 0 || !check_dtype(dtype)) return set_err(FX_E_ARG, "bad synth args");
+    DeviceGuard g(device);
+    if (!g.ok) return set_err(FX_E_HIP, "hipSetDevice(%d) failed", device);
+    HIP_TRY(launch_synth(out, row0, n, d, dtype, seed, (hipStream_t)stream));
+    return FX_OK;
+}
+
+int fx_index_profile(FxIndex* h, int enable) {
+    if (!h) return set_err(FX_E_ARG, "null index");
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard g(h->device);
+    HIP_TRY(hipStreamSynchronize(h->stream()));
+    for (auto& pr : h->ev_scan) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
+    for (auto& pr : h->ev_merge) (void)hipEventDestroy(pr.second);
+    h->ev_scan.clear();
+    h->ev_merge.clear();
+    h->profile = enable != 0;
+    return FX_OK;
+}
+
+int fx_index_profile_read(FxIndex* h, double* scan_ms, double* merge_ms, int64_t* launches) {
+    if (!h || !scan_ms || !merge_ms || !launches) return set_err(FX_E_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(h->mu);
+    DeviceGuard g(h->device);
+    HIP_TRY(hipStreamSynchronize(h->stream()));
+    double a = 0, b = 0;
+    for (size_t i = 0; i < h->ev_scan.size(); ++i) {
+        float ms = 0;
+        HIP_TRY(hipEventElapsedTime(&ms, h->ev_scan[i].first, h->ev_scan[i].second));
+        a += ms;
+        HIP_TRY(hipEventElapsedTime(&ms, h->ev_merge[i].first, h->ev_merge[i].second));
+        b += ms;
+    }
+    *scan_ms = a;
+    *merge_ms = b;
+    *launches = (int64_t)h->ev_scan.size();
+    return FX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,87 @@
+// fx_internal.h -- shared between the HIP kernels (fx_kernels.hip) and the
+// host C ABI (fx_index.cpp).  Not part of the public ABI (include/fx_index.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fx {
+
+// ---- tiling of the fused scan kernel (see DESIGN.md "scan kernel") --------
+constexpr int TILE_R = 128;   // corpus rows per tile (MFMA M side)
+constexpr int TILE_Q = 128;   // queries per tile      (MFMA N side)
+constexpr int STAGE_B = 128;  // bytes of each row's K staged per pipeline stage
+constexpr int KP = 32;        // candidates kept per (query, corpus split)
+constexpr int CAP = 64;       // LDS candidate-list capacity per query (2*KP)
+constexpr int ROW_ALIGN = 128;  // row stride alignment in bytes (== STAGE_B)
+constexpr int SCAN_THREADS = 256;
+
+// dynamic LDS carve of the scan kernel (all in ONE extern array: see
+// cdna_hip_programming.md 5.4 item 4(a))
+constexpr int LDS_STAGE = 2 * (TILE_R + TILE_Q) * STAGE_B;   // 64 KiB double buffer
+constexpr int LDS_NORM_OFF = LDS_STAGE;                       // 2 x 512 B row norms
+constexpr int LDS_LD_OFF = LDS_NORM_OFF + 2 * TILE_R * 4;    // lst_d [TILE_Q][CAP] f32
+constexpr int LDS_LI_OFF = LDS_LD_OFF + TILE_Q * CAP * 4;    // lst_i [TILE_Q][CAP] i32
+constexpr int LDS_CNT_OFF = LDS_LI_OFF + TILE_Q * CAP * 4;   // cnt   [TILE_Q] i32
+constexpr int LDS_TAU_OFF = LDS_CNT_OFF + TILE_Q * 4;        // tau   [TILE_Q] f32
+constexpr int LDS_FLAG_OFF = LDS_TAU_OFF + TILE_Q * 4;       // overflow flag (16 B)
+constexpr int LDS_SCAN_BYTES = LDS_FLAG_OFF + 16;
+
+enum Dtype { F32 = 0, BF16 = 1, F16 = 2 };
+enum Metric { IP = 0, L2 = 1 };
+
+inline int dtype_size(int dt) { return dt == F32 ? 4 : 2; }
+
+struct ScanParams {
+    const char* codes;     // [cap_rows][row_bytes] storage dtype, zero padded
+    const float* norms;    // [cap_rows] |y|^2 (fp32, of stored values)
+    int64_t ntotal;
+    int row_bytes;
+    const char* qop;       // [nq_pad][row_bytes] queries in storage dtype
+    int64_t nq;
+    int n_qtiles;
+    int n_ctiles;          // corpus tiles (ceil(ntotal / TILE_R))
+    int splits;            // corpus splits per query tile
+    int qt_per_xcd;        // query tiles assigned per XCD group
+    float* cand_d;         // [n_qtiles][splits][TILE_Q][KP]
+    int* cand_i;
+};
+
+struct RefineParams {
+    const float* cand_d;   // scan output (approx keys)
+    const int* cand_i;
+    int splits;
+    int64_t nq;
+    int k;
+    const char* codes;
+    int row_bytes;
+    int kdim;
+    const float* qf32;     // [nq_pad][kdim] fp32 queries, zero padded
+    const float* qeps;     // [nq] certification margin
+    int64_t id_offset;
+    float* D;              // [nq][k]
+    int64_t* I;
+    int* n_flag;           // uncertified counter
+    int* flag_list;        // [nq] uncertified query ids
+};
+
+// launchers (stream-ordered, no host sync) -- fx_kernels.hip
+hipError_t launch_convert_rows(const void* x, int x_dt, int64_t n, int d, void* codes_row0, int st_dt,
+                               int kdim, float* norms_row0, unsigned* max_sq_bits, int normalize,
+                               hipStream_t s);
+hipError_t launch_prep_queries(const void* q, int q_dt, int64_t nq, int64_t nq_pad, int d, int kdim,
+                               int st_dt, int metric, float* qf32, void* qop, float* qeps,
+                               double max_norm, hipStream_t s);
+hipError_t launch_scan(int st_dt, int metric, const ScanParams& p, hipStream_t s);
+hipError_t launch_refine(int st_dt, int metric, const RefineParams& p, hipStream_t s);
+hipError_t launch_exact_fallback(int st_dt, int metric, const char* codes, int row_bytes, int kdim,
+                                 int64_t ntotal, const float* qf32, const int* qlist, int nlist,
+                                 int k, int64_t id_offset, float* cand_d, int* cand_i, int fb_splits,
+                                 float* D, int64_t* I, hipStream_t s);
+hipError_t launch_merge_shards(int metric, int nshards, int64_t nq, int k, const float* D_in,
+                               const int64_t* I_in, float* D_out, int64_t* I_out, hipStream_t s);
+hipError_t launch_synth(void* out, int64_t row0, int64_t n, int d, int dtype, uint64_t seed,
+                        hipStream_t s);
+hipError_t launch_to_f32(const void* codes, int st_dt, int row_bytes, int64_t n, int d, float* out,
+                         hipStream_t s);
+
+}  // namespace fx

@@ -76,7 +76,9 @@ void fx_index_free(FxIndex* index);
  * reference default is off: SURVEY.md section 8a a8). */
 int fx_index_set_normalize(FxIndex* index, int on);
 /* Run the index's kernels on `stream` (a hipStream_t; NULL = the index's own
- * stream).  Lets a caller order index work after its own producers. */
+ * stream, which is a blocking stream and therefore ordered with work on the
+ * legacy null stream).  Lets a caller order index work after its own
+ * producers. */
 int fx_index_set_stream(FxIndex* index, void* stream);
 /* Global id of local row 0 (row-sharded multi-GPU: shard offset). */
 int fx_index_set_id_offset(FxIndex* index, int64_t offset);

@@ -18,6 +18,15 @@ if not LIB_PATH.exists():
         f"{LIB_PATH} not found: the MI355X HIP library is required (build it with "
         f"`make -C {_HERE / 'csrc'}`); there is no CPU fallback")
 
+# One HIP runtime per process: torch ships its own libamdhip64 (SONAME
+# libamdhip64.so.7, like /opt/rocm's).  Loaded first, torch's copy satisfies
+# our NEEDED entry and both share it; loaded second, torch would pull a second
+# runtime that sees no device.  So bring torch in first when it is installed.
+try:  # pragma: no cover - torch is part of the image
+    import torch  # noqa: F401
+except Exception:  # noqa: BLE001
+    pass
+
 lib = ctypes.CDLL(str(LIB_PATH))
 
 F32, BF16, F16 = 0, 1, 2

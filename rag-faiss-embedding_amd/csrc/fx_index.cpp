@@ -299,7 +299,10 @@ int fx_index_create(int d, int storage_dtype, int metric, int device, FxIndex** 
     h->device = device;
     h->row_bytes = (int)round_up((int64_t)d * dtype_size(storage_dtype), ROW_ALIGN);
     h->kdim = h->row_bytes / dtype_size(storage_dtype);
-    hipError_t e = hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking);
+    // A BLOCKING stream: work on the legacy null stream (torch's default
+    // stream, cuda_stream == 0) is ordered before and after it, so a caller
+    // that binds "stream 0" (fx_index_set_stream(h, NULL)) stays ordered.
+    hipError_t e = hipStreamCreateWithFlags(&h->own_stream, hipStreamDefault);
     if (e == hipSuccess) e = hipMalloc(&h->max_sq_bits, 16);
     if (e == hipSuccess) e = hipMemset(h->max_sq_bits, 0, 16);
     if (e != hipSuccess) {

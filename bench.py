@@ -1,0 +1,281 @@
+#!/usr/bin/env python3
+"""Headline benchmark: queries/sec + recall@10 of exact flat-L2 search.
+
+BASELINE.json metric: "queries/sec + recall@10 vs CPU FAISS, 10M x 768 flat
+index, 1/2/4/8 MI355X".  Default workload = BASELINE config (d): a 10M x 768
+bf16 corpus row-sharded over the N GPUs of one node (one process per GPU),
+10,000-query batches, k = 10; each rank scans its shard (fused MFMA GEMM +
+top-k kernel), the per-shard top-k lists are exchanged with one RCCL
+all_gather over xGMI and merged on device.  The total corpus is fixed, so
+scaling is "strong".
+
+One step = one search of one 10k-query batch (queries already resident in
+HBM; results left in HBM).  Corpus and queries are synthetic (counter-hash
+generator shared with oracle/flat_l2.c, exact in bf16), generated on the GPU.
+
+Launch: python bench.py [--gpus 1 --steps 10 --warmup 2]   (N=1)
+        python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+import torch  # noqa: E402  (before the HIP library: one runtime per process)
+import torch.distributed as dist  # noqa: E402
+
+import amd_fx  # noqa: E402,F401
+from rag_faiss_embedding_amd import faiss as fx  # noqa: E402
+
+METRIC = "queries/sec + recall@10 vs CPU FAISS, 10M×768 flat index, 1/2/4/8 MI355X"
+CORPUS_SEED, QUERY_SEED = 1234, 4321
+
+# BASELINE.json configs usable as bench workloads (name -> rows, dim, dtype, nq, k)
+CONFIGS = {
+    "d": (10_000_000, 768, "bfloat16", 10_000, 10),   # the headline (metric's config)
+    "b": (1_000_000, 384, "float32", 1_000, 10),
+    "e": (100_000_000, 384, "float16", 10_000, 10),
+}
+TORCH_DT = {"float32": torch.float32, "bfloat16": torch.bfloat16, "float16": torch.float16}
+SHORT_DT = {"float32": "f32", "bfloat16": "bf16", "float16": "f16"}
+# MI355X_MICROARCH.md: dense MFMA peaks (TFLOP/s) and HBM3E peak (GB/s)
+MFMA_PEAK = {"float32": 157.3, "bfloat16": 2500.0, "float16": 2500.0}
+HBM_PEAK_GBS = 8000.0
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def build_shard(ix, rank, world, n_total, d, dtype, device):
+    lo = n_total * rank // world
+    hi = n_total * (rank + 1) // world
+    ix.reserve(hi - lo)
+    chunk = 1 << 20
+    buf = torch.empty((min(chunk, hi - lo), d), dtype=TORCH_DT[dtype], device=device)
+    for r0 in range(lo, hi, chunk):
+        nr = min(chunk, hi - r0)
+        part = buf[:nr]
+        fx.synth_fill(part, r0, CORPUS_SEED)
+        ix.add(part)
+    ix.set_id_offset(lo)
+    torch.cuda.synchronize()
+    return lo, hi
+
+
+def one_step(ix, xq, k, world, gath):
+    D, I = ix.search(xq, k)
+    if world == 1:
+        return D, I
+    Dg, Ig = gath
+    dist.all_gather_into_tensor(Dg.view(-1, k), D)
+    dist.all_gather_into_tensor(Ig.view(-1, k), I)
+    return fx.merge_shards(ix.metric_type, Dg, Ig, k)
+
+
+def oracle_lib_native():
+    """Compile oracle/flat_l2.c for THIS host (-march=native) into a temp dir;
+    fall back to the prebuilt x86-64-v3 library."""
+    from oracle import cpu as C
+    try:
+        out = Path(tempfile.mkdtemp(prefix="fx_oracle_"))
+        p = C.build(arch="-march=native", out_dir=out)
+        return C, C.load(p), "-march=native"
+    except Exception as e:  # noqa: BLE001
+        log("native oracle build failed, using prebuilt:", e)
+        return C, C.load(), "-march=x86-64-v3"
+
+
+def cpu_baseline_and_recall(args, n_total, d, k, D, I, nthreads):
+    """cpu_baseline leg (rank 0): the repo's C/OpenMP restatement of FAISS's
+    IndexFlatL2 BLAS path timed on a bounded sample of the same workload, and
+    recall@10 of the GPU result against the exact CPU oracle on a query
+    sample over the FULL corpus."""
+    import numpy as np
+    C, lib, march = oracle_lib_native()
+    res = {}
+    # recall: exact streaming oracle (rows regenerated on the fly) vs GPU ids
+    nr = min(args.recall_queries, D.shape[0])
+    qsel = np.linspace(0, D.shape[0] - 1, nr).astype(np.int64)
+    from oracle import flat_l2 as F
+    xq = np.concatenate([F.synth(QUERY_SEED, int(q), 1, d) for q in qsel])
+    t0 = time.time()
+    Dr, Ir = C.knn_exact_synth(CORPUS_SEED, n_total, d, xq, k, nthreads)
+    t_rec = time.time() - t0
+    Ig = I[qsel].cpu().numpy()
+    Dgpu = D[qsel].cpu().numpy()
+    hits = sum(len(set(Ig[i].tolist()) & set(Ir[i].tolist())) for i in range(nr))
+    res["recall_at_10"] = hits / float(nr * k)
+    res["ids_bit_exact"] = bool((Ig == Ir).all())
+    res["max_rel_dist_err"] = float(np.max(np.abs(Dgpu.astype(np.float64) - Dr) / np.maximum(1.0, np.abs(Dr))))
+    res["recall_sample"] = f"{nr} queries x full {n_total}-row corpus, exact CPU oracle ({t_rec:.1f}s)"
+    # timed baseline: BLAS-path port on a corpus slice, extrapolated to n_total
+    rows = min(n_total, args.cpu_rows)
+    nq_s = args.cpu_queries
+    xb = C.synth(CORPUS_SEED, 0, rows, d, nthreads)
+    xqs = C.synth(QUERY_SEED, 0, nq_s, d, nthreads)
+    C.knn_blas(xqs[:8], xb[:4096], k, nthreads, lib=lib)  # warm
+    t0 = time.time()
+    C.knn_blas(xqs, xb, k, nthreads, lib=lib)
+    t = time.time() - t0
+    qps = nq_s / (t * (n_total / rows))
+    res["cpu_baseline"] = {
+        "value": qps, "unit": "queries/s", "cores": nthreads, "kind": "port",
+        "sample": (f"{nq_s} queries x first {rows} rows (fp32) of the same corpus in {t:.2f}s, "
+                   f"extrapolated linearly to {n_total} rows; C/OpenMP restatement of faiss "
+                   f"IndexFlatL2 BLAS path (oracle/flat_l2.c, {march}); faiss-cpu is not installed"),
+    }
+    return res
+
+
+def read_pmc_traffic(cfg_name, n_local, nq):
+    """HBM bytes per scan launch from a committed rocprofv3 --pmc summary of
+    this same workload (profiles/*_pmc_scan.json), or None."""
+    p = ROOT / "profiles" / f"pmc_scan_{cfg_name}.json"
+    if not p.exists():
+        return None
+    try:
+        j = json.loads(p.read_text())
+        if j.get("rows_per_gpu") == n_local and j.get("nq") == nq:
+            return j.get("hbm_bytes_per_launch")
+    except Exception:  # noqa: BLE001
+        return None
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="d", choices=sorted(CONFIGS))
+    ap.add_argument("--nq", type=int, default=0, help="override query batch")
+    ap.add_argument("--rows", type=int, default=0, help="override corpus rows (testing)")
+    ap.add_argument("--recall-queries", type=int, default=32)
+    ap.add_argument("--cpu-rows", type=int, default=1_000_000)
+    ap.add_argument("--cpu-queries", type=int, default=1000)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline / recall leg")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=device)
+
+    n_total, d, dtype, nq, k = CONFIGS[args.config]
+    if args.nq:
+        nq = args.nq
+    if args.rows:
+        n_total = args.rows
+
+    t0 = time.time()
+    ix = fx.IndexFlatL2(d, dtype=dtype, device=local)
+    lo, hi = build_shard(ix, rank, world, n_total, d, dtype, device)
+    n_local = hi - lo
+    xq = torch.empty((nq, d), dtype=TORCH_DT[dtype], device=device)
+    fx.synth_fill(xq, 0, QUERY_SEED)
+    gath = None
+    if world > 1:
+        gath = (torch.empty((world, nq, k), dtype=torch.float32, device=device),
+                torch.empty((world, nq, k), dtype=torch.int64, device=device))
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] shard rows [{lo}, {hi}) built in {time.time() - t0:.1f}s")
+
+    for _ in range(args.warmup):
+        one_step(ix, xq, k, world, gath)
+    ix.profile(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        D, I = one_step(ix, xq, k, world, gath)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    scan_ms, merge_ms, launches = ix.profile_read()
+    ix.profile(False)
+    fallbacks = ix.last_fallbacks()
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        ts = torch.tensor([scan_ms / max(launches, 1)], dtype=torch.float64, device=device)
+        dist.all_reduce(ts, op=dist.ReduceOp.MAX)
+        scan_avg_ms = float(ts.item())
+    else:
+        scan_avg_ms = scan_ms / max(launches, 1)
+
+    value = nq * args.steps / elapsed
+    # roofline of the dominant kernel (the fused scan): algorithmic work per launch
+    flops = 2.0 * nq * n_local * d
+    esize = 4 if dtype == "float32" else 2
+    alg_bytes = n_local * d * esize + nq * d * esize + nq * k * 12
+    t_scan = scan_avg_ms / 1e3
+    mfma_tf = flops / t_scan / 1e12
+    ridge = MFMA_PEAK[dtype] * 1e12 / (HBM_PEAK_GBS * 1e9)
+    if flops / alg_bytes >= ridge:
+        roof = {"bound": "mfma", "achieved": round(mfma_tf, 2), "peak": MFMA_PEAK[dtype], "unit": "TFLOP/s",
+                "frac": round(mfma_tf / MFMA_PEAK[dtype], 4)}
+    else:
+        gbs = alg_bytes / t_scan / 1e9
+        roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    roof["traffic"] = read_pmc_traffic(args.config, n_local, nq)
+    roof["kernel"] = "k_scan_topk (fused MFMA distance GEMM + top-k)"
+    roof["kernel_ms_avg"] = round(scan_avg_ms, 4)
+    roof["launches"] = launches
+    roof["merge_refine_ms_avg"] = round(merge_ms / max(launches, 1), 4)
+
+    out = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "queries/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": SHORT_DT[dtype],
+        "data": "synthetic: counter-hash corpus/queries generated on the GPU (exact in bf16/fp16/fp32)",
+        "config": {
+            "workload": (f"{n_total} x {d} {SHORT_DT[dtype]} flat L2 index, {nq}-query batch, top-{k}, "
+                         f"row-sharded over {world} GPU(s) + RCCL all_gather merge"),
+            "baseline_config": args.config, "corpus_rows": n_total, "dim": d, "nq": nq, "k": k,
+            "rows_per_gpu": n_local, "parallelism": f"row-shard x{world}",
+        },
+        "fallback_queries_last_step": fallbacks,
+        "roofline": roof,
+    }
+    if rank == 0 and not args.no_cpu:
+        nthreads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+        extra = cpu_baseline_and_recall(args, n_total, d, k, D, I, nthreads)
+        if world > 1:
+            extra.pop("cpu_baseline", None)
+        out.update(extra)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

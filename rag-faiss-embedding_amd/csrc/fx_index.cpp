@@ -119,7 +119,8 @@ hipError_t grow(FxIndex* h, int64_t need_rows) {
     hipStream_t s = h->stream();
     // zero-fill: padding rows of the last tile must be finite
     e = hipMemsetAsync(codes + (size_t)h->ntotal * h->row_bytes, 0, (size_t)(cap - h->ntotal) * h->row_bytes, s);
-    if (e == hipSuccess) e = hipMemsetAsync(norms + h->ntotal, 0, (size_t)(cap - h->ntotal) * sizeof(float), s);
+    // padding rows: |y|^2 = +inf keeps them out of the scan's candidate lists
+    if (e == hipSuccess) e = hipMemsetD32Async((hipDeviceptr_t)(norms + h->ntotal), 0x7f800000u, (size_t)(cap - h->ntotal), s);
     if (e == hipSuccess && h->ntotal > 0) {
         e = hipMemcpyAsync(codes, h->codes, (size_t)h->ntotal * h->row_bytes, hipMemcpyDeviceToDevice, s);
         if (e == hipSuccess)
@@ -462,7 +463,7 @@ int fx_index_reset(FxIndex* h) {
     HIP_TRY(hipMemset(h->max_sq_bits, 0, 4));
     if (h->codes && h->cap_rows > 0) {
         HIP_TRY(hipMemset(h->codes, 0, (size_t)h->cap_rows * h->row_bytes));
-        HIP_TRY(hipMemset(h->norms, 0, (size_t)h->cap_rows * sizeof(float)));
+        HIP_TRY(hipMemsetD32((hipDeviceptr_t)h->norms, 0x7f800000u, (size_t)h->cap_rows));
     }
     h->max_sq = 0.0f;
     h->ntotal = 0;

@@ -28,6 +28,7 @@
 
 #include <float.h>
 #include <limits.h>
+#include <stdlib.h>
 
 namespace fx {
 
@@ -454,6 +455,343 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_topk(ScanParams p) {
 }
 
 // ---------------------------------------------------------------------------
+// scan kernel v2: queries stationary in VGPRs, corpus streamed through a
+// 5-deep global_load_lds ring (counted vmcnt, one raw barrier per stage)
+// ---------------------------------------------------------------------------
+//
+// Workgroup = 4 waves = 128 queries (32 per wave, held as MFMA B fragments for
+// the whole K: KSTEPS x 2 fragments, <= 192 VGPRs) x a corpus split streamed in
+// 128-row tiles.  Per 128-B stage every wave issues exactly 4 corpus LDS-DMA
+// pieces + 1 norm piece, so `s_waitcnt vmcnt(5*(NS-2))` retires exactly the
+// stage about to be read (stages past the split end re-read the last tile to
+// keep the count uniform).  All 4 waves read the same 16 A fragments per stage
+// (LDS: 64 KiB per 512 MFMA cycles); only the corpus crosses L2 (16 KiB/stage).
+
+// MFMA with the (stationary) B operand pinned in AGPRs via inline asm: the
+// builtin form leaves the 192 query VGPRs to the allocator, which spills them.
+// hipcc does not know the latency of an asm MFMA, so (a) a tile's first MFMA
+// uses the srcC = 0 form (no VALU zeroing of the accumulator -> no VALU->MFMA
+// hazard) and (b) acc_fence() pads 24 wait states (>= the 19 an XDL write ->
+// VALU read needs) and is tied to every accumulator before the epilogue reads.
+template <int DT> struct AsmMma;
+template <> struct AsmMma<BF16> {
+    typedef bf16x8 A;
+    typedef bf16x8 B;
+    static __device__ __forceinline__ void mma(f32x4& c, const A& a, const B& b) {
+        asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "a"(b));
+    }
+    static __device__ __forceinline__ void mma0(f32x4& c, const A& a, const B& b) {
+        asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=v"(c) : "v"(a), "a"(b));
+    }
+};
+template <> struct AsmMma<F16> {
+    typedef f16x8 A;
+    typedef f16x8 B;
+    static __device__ __forceinline__ void mma(f32x4& c, const A& a, const B& b) {
+        asm("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "a"(b));
+    }
+    static __device__ __forceinline__ void mma0(f32x4& c, const A& a, const B& b) {
+        asm("v_mfma_f32_16x16x32_f16 %0, %1, %2, 0" : "=v"(c) : "v"(a), "a"(b));
+    }
+};
+// f32: a 64-B k-chunk is 4 k-steps of 16x16x4 (see Frag<F32>); B is kept as 4
+// scalar AGPRs per chunk.
+struct Bf32 { float x[4]; };
+template <> struct AsmMma<F32> {
+    typedef f32x4 A;
+    typedef Bf32 B;
+    static __device__ __forceinline__ void mma(f32x4& c, const A& a, const B& b) {
+        asm("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(c) : "v"(a[0]), "a"(b.x[0]));
+        asm("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(c) : "v"(a[1]), "a"(b.x[1]));
+        asm("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(c) : "v"(a[2]), "a"(b.x[2]));
+        asm("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(c) : "v"(a[3]), "a"(b.x[3]));
+    }
+    static __device__ __forceinline__ void mma0(f32x4& c, const A& a, const B& b) {
+        asm("v_mfma_f32_16x16x4_f32 %0, %1, %2, 0" : "=v"(c) : "v"(a[0]), "a"(b.x[0]));
+        asm("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(c) : "v"(a[1]), "a"(b.x[1]));
+        asm("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(c) : "v"(a[2]), "a"(b.x[2]));
+        asm("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(c) : "v"(a[3]), "a"(b.x[3]));
+    }
+};
+
+// LDS byte offset of a generic pointer into the extern LDS array
+__device__ __forceinline__ uint32_t lds_off(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+// The epilogue's per-tile LDS reads (row norms, tau, flag) as inline asm: hipcc
+// would otherwise treat them as possibly aliasing the in-flight LDS-DMA ring and
+// drain it with s_waitcnt vmcnt(0) once per tile.  Their data is ordered by the
+// stage's counted vmcnt + barrier (norms) or by the previous barrier (tau, flag).
+__device__ __forceinline__ void lds_read_epi(const float* norm_base, const float* tau_base, f32x4 (&y)[8],
+                                             float (&t)[2]) {
+    asm volatile(
+        "ds_read_b128 %0, %10\n\t"
+        "ds_read_b128 %1, %10 offset:64\n\t"
+        "ds_read_b128 %2, %10 offset:128\n\t"
+        "ds_read_b128 %3, %10 offset:192\n\t"
+        "ds_read_b128 %4, %10 offset:256\n\t"
+        "ds_read_b128 %5, %10 offset:320\n\t"
+        "ds_read_b128 %6, %10 offset:384\n\t"
+        "ds_read_b128 %7, %10 offset:448\n\t"
+        "ds_read_b32 %8, %11\n\t"
+        "ds_read_b32 %9, %11 offset:64\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(y[0]), "=&v"(y[1]), "=&v"(y[2]), "=&v"(y[3]), "=&v"(y[4]), "=&v"(y[5]), "=&v"(y[6]), "=&v"(y[7]),
+          "=&v"(t[0]), "=&v"(t[1])
+        : "v"(lds_off(norm_base)), "v"(lds_off(tau_base))
+        : "memory");
+}
+__device__ __forceinline__ int lds_read_flag(const volatile int* f) {
+    int v;
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_off((const void*)f)) : "memory");
+    return v;
+}
+
+template <int M>
+__device__ __forceinline__ void acc_fence(f32x4 (&acc)[M][2]) {
+    static_assert(M == 8, "acc_fence operand list is written for 8x2 accumulators");
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7"
+                 : "+v"(acc[0][0]), "+v"(acc[0][1]), "+v"(acc[1][0]), "+v"(acc[1][1]), "+v"(acc[2][0]),
+                   "+v"(acc[2][1]), "+v"(acc[3][0]), "+v"(acc[3][1]), "+v"(acc[4][0]), "+v"(acc[4][1]),
+                   "+v"(acc[5][0]), "+v"(acc[5][1]), "+v"(acc[6][0]), "+v"(acc[6][1]), "+v"(acc[7][0]),
+                   "+v"(acc[7][1]));
+}
+
+constexpr int V2_NS = 5;
+constexpr int V2_STAGE = TILE_R * STAGE_B;                     // 16 KiB
+constexpr int V2_NORM_OFF = V2_NS * V2_STAGE;                  // 4 slots x 512 B
+constexpr int V2_LD_OFF = V2_NORM_OFF + 4 * TILE_R * 4;
+constexpr int V2_LI_OFF = V2_LD_OFF + TILE_Q * CAP * 4;
+constexpr int V2_CNT_OFF = V2_LI_OFF + TILE_Q * CAP * 4;
+constexpr int V2_TAU_OFF = V2_CNT_OFF + TILE_Q * 4;
+constexpr int V2_FLAG_OFF = V2_TAU_OFF + TILE_Q * 4;
+constexpr int V2_LDS_BYTES = V2_FLAG_OFF + 16;
+static_assert(V2_LDS_BYTES <= 160 * 1024, "LDS budget");
+
+// push the tile's survivors (key <= tau) into the LDS lists; elements that
+// find their list full stay pending (bit set) for the overflow path
+template <int M, int N, int METRIC>
+__device__ __forceinline__ bool epi_push(const f32x4 (&acc)[M][N], const float (&yn)[M][4], const int (&qloc)[N],
+                                         const float (&tn)[N], int rl0, int rlim, int trow0, unsigned (&pend)[N],
+                                         float* lst_d, int* lst_i, int* cnt) {
+    // fast reject: per query the smallest key of the tile (padding rows carry
+    // |y|^2 = +inf, so they only reach the exact checks below while tau = inf)
+    bool any = false;
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+        float mn = FX_INF;
+#pragma unroll
+        for (int m = 0; m < M; ++m)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                mn = fminf(mn, METRIC == L2 ? fmaf(-2.0f, acc[m][n][i], yn[m][i]) : -acc[m][n][i]);
+        any |= mn <= tn[n];
+    }
+    if (!__any(any)) return false;
+    bool ovf = false;
+#pragma unroll
+    for (int n = 0; n < N; ++n)
+#pragma unroll
+        for (int m = 0; m < M; ++m)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float v = METRIC == L2 ? fmaf(-2.0f, acc[m][n][i], yn[m][i]) : -acc[m][n][i];
+                const int rl = rl0 + m * 16 + i;
+                if (rl < rlim && v <= tn[n]) {
+                    const int s = atomicAdd(&cnt[qloc[n]], 1);
+                    if (s < CAP) {
+                        lst_d[qloc[n] * CAP + s] = v;
+                        lst_i[qloc[n] * CAP + s] = trow0 + rl;
+                    } else {
+                        pend[n] |= 1u << (m * 4 + i);
+                        ovf = true;
+                    }
+                }
+            }
+    return ovf;
+}
+
+template <int M, int N, int METRIC>
+__device__ __forceinline__ bool epi_retry(const f32x4 (&acc)[M][N], const float (&yn)[M][4], const int (&qloc)[N],
+                                          const float (&tn)[N], int rl0, int trow0, unsigned (&pend)[N],
+                                          float* lst_d, int* lst_i, int* cnt) {
+    bool ovf = false;
+#pragma unroll
+    for (int n = 0; n < N; ++n)
+#pragma unroll
+        for (int m = 0; m < M; ++m)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const unsigned bit = 1u << (m * 4 + i);
+                if (pend[n] & bit) {
+                    const float v = METRIC == L2 ? fmaf(-2.0f, acc[m][n][i], yn[m][i]) : -acc[m][n][i];
+                    pend[n] &= ~bit;
+                    if (v <= tn[n]) {
+                        const int s = atomicAdd(&cnt[qloc[n]], 1);
+                        if (s < CAP) {
+                            lst_d[qloc[n] * CAP + s] = v;
+                            lst_i[qloc[n] * CAP + s] = trow0 + rl0 + m * 16 + i;
+                        } else {
+                            pend[n] |= bit;
+                            ovf = true;
+                        }
+                    }
+                }
+            }
+    return ovf;
+}
+
+template <int DT, int METRIC, int KSTEPS>
+__global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_qreg(ScanParams p) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    typedef typename AsmMma<DT>::A frag_t;
+    constexpr int SPT = KSTEPS / 2;  // 128-B stages per tile
+    constexpr int NS = V2_NS;
+    constexpr int M = TILE_R / 16;   // 8 row blocks per tile
+    constexpr int N = 2;             // 2 query blocks of 16 per wave
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int qtile, split;
+    map_block(blockIdx.x, p, qtile, split);
+    if (qtile >= p.n_qtiles) return;
+    const int ct0 = (int)((int64_t)split * p.n_ctiles / p.splits);
+    const int ct1 = (int)((int64_t)(split + 1) * p.n_ctiles / p.splits);
+    const int ntiles = ct1 - ct0;
+    const int64_t q0 = (int64_t)qtile * TILE_Q;
+    constexpr int rb = KSTEPS * 64;
+
+    float* lst_d = (float*)(smem + V2_LD_OFF);
+    int* lst_i = (int*)(smem + V2_LI_OFF);
+    int* cnt = (int*)(smem + V2_CNT_OFF);
+    float* tau = (float*)(smem + V2_TAU_OFF);
+    volatile int* flag = (volatile int*)(smem + V2_FLAG_OFF);
+    for (int x = tid; x < TILE_Q; x += SCAN_THREADS) { cnt[x] = 0; tau[x] = FX_INF; }
+    if (tid == 0) *flag = 0;
+
+    // this wave's 32 queries as B fragments for every k-step (stationary, AGPRs)
+    typedef typename AsmMma<DT>::B bfrag_t;
+    bfrag_t b[KSTEPS][N];
+    {
+        const char* qb = p.qop + (q0 + wave * 32 + (lane & 15)) * rb + (lane >> 4) * 16;
+#pragma unroll
+        for (int ks = 0; ks < KSTEPS; ++ks)
+#pragma unroll
+            for (int n = 0; n < N; ++n) b[ks][n] = *(const bfrag_t*)(qb + n * 16 * rb + ks * 64);
+    }
+    int offs[4];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+        const int bi = wave * 4 + jj, rblk = bi >> 1, kb = bi & 1;
+        offs[jj] = (rblk * 16 + (lane & 15)) * rb + kb * 64 + (lane >> 4) * 16;
+    }
+    auto issue = [&](int g) {
+        int t = g / SPT;
+        const int j = g - t * SPT;
+        if (t >= ntiles) t = ntiles - 1;  // dummy stage: uniform vmcnt accounting
+        const int64_t row0 = (int64_t)(ct0 + t) * TILE_R;
+        char* slot = smem + (g % NS) * V2_STAGE;
+        const char* src = p.codes + row0 * rb + j * STAGE_B;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) glds16(src + offs[jj], slot + (wave * 4 + jj) * 1024);
+        if (lane < 8) glds16(p.norms + row0 + wave * 32 + lane * 4, smem + V2_NORM_OFF + (t & 3) * 512 + wave * 128);
+    };
+
+#pragma unroll
+    for (int s = 0; s < NS - 1; ++s) issue(s);
+
+    f32x4 acc[M][N];
+    const int rl0 = 4 * (lane >> 4);
+    int qloc[N];
+#pragma unroll
+    for (int n = 0; n < N; ++n) qloc[n] = wave * 32 + n * 16 + (lane & 15);
+    const bool qv0 = q0 + qloc[0] < p.nq, qv1 = q0 + qloc[1] < p.nq;
+    unsigned pend[N] = {0u, 0u};
+
+    // slow path: compact full lists and re-push pending survivors of tile `tp`
+    auto overflow = [&](int tp) {
+        const float* nb = (const float*)(smem + V2_NORM_OFF + (tp & 3) * 512);
+        float yn[M][4];
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            const float4 v = *(const float4*)(nb + rl0 + m * 16);
+            yn[m][0] = v.x; yn[m][1] = v.y; yn[m][2] = v.z; yn[m][3] = v.w;
+        }
+        const int trow0 = (ct0 + tp) * TILE_R;
+        while (*flag) {
+            __syncthreads();
+            if (tid == 0) *flag = 0;
+            compact_full(lst_d, lst_i, cnt, tau, wave, lane);
+            __syncthreads();
+            float tn[N];
+#pragma unroll
+            for (int n = 0; n < N; ++n) tn[n] = tau[qloc[n]];
+            if (epi_retry<M, N, METRIC>(acc, yn, qloc, tn, rl0, trow0, pend, lst_d, lst_i, cnt)) *flag = 1;
+            __syncthreads();
+        }
+    };
+
+    for (int t = 0; t < ntiles; ++t) {
+        // K loop of one 128-row tile, fully unrolled (B fragments are indexed
+        // by k-step: must be compile-time to stay in registers)
+#pragma unroll
+        for (int j = 0; j < SPT; ++j) {
+            const int g = t * SPT + j;
+            asm volatile("s_waitcnt vmcnt(15) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            issue(g + NS - 1);
+            const char* slot = smem + (g % NS) * V2_STAGE;
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb) {
+                frag_t a[M];
+#pragma unroll
+                for (int m = 0; m < M; ++m) a[m] = *(const frag_t*)(slot + (m * 2 + kb) * 1024 + lane * 16);
+#pragma unroll
+                for (int m = 0; m < M; ++m)
+#pragma unroll
+                    for (int n = 0; n < N; ++n) {
+                        if (j == 0 && kb == 0) AsmMma<DT>::mma0(acc[m][n], a[m], b[0][n]);
+                        else AsmMma<DT>::mma(acc[m][n], a[m], b[2 * j + kb][n]);
+                    }
+            }
+        }
+        // epilogue: filter against tau, push survivors into the LDS lists
+        acc_fence<M>(acc);
+        {
+            const float* nb = (const float*)(smem + V2_NORM_OFF + (t & 3) * 512);
+            f32x4 y4[M];
+            float tn[N];
+            lds_read_epi(nb + rl0, tau + qloc[0], y4, tn);
+            float yn[M][4];
+#pragma unroll
+            for (int m = 0; m < M; ++m) {
+                yn[m][0] = y4[m][0]; yn[m][1] = y4[m][1]; yn[m][2] = y4[m][2]; yn[m][3] = y4[m][3];
+            }
+            if (!qv0) tn[0] = -FX_INF;
+            if (!qv1) tn[1] = -FX_INF;
+            const int trow0 = (ct0 + t) * TILE_R;
+            const int rlim = (int)(p.ntotal - (int64_t)trow0);
+            if (epi_push<M, N, METRIC>(acc, yn, qloc, tn, rl0, rlim, trow0, pend, lst_d, lst_i, cnt)) *flag = 1;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (lds_read_flag(flag)) overflow(t);
+    }
+    // final flush: sorted top-KP per query of this (query tile, split)
+    __syncthreads();
+    const int64_t obase = ((int64_t)qtile * p.splits + split) * TILE_Q;
+    for (int q = wave; q < TILE_Q; q += 4) {
+        if (q0 + q >= p.nq) break;
+        const int c = min(cnt[q], CAP);
+        float d = lane < c ? lst_d[q * CAP + lane] : FX_INF;
+        int i = lane < c ? lst_i[q * CAP + lane] : INT_MAX;
+        sort64(d, i, lane);
+        if (lane < KP) {
+            p.cand_d[(obase + q) * KP + lane] = d;
+            p.cand_i[(obase + q) * KP + lane] = i == INT_MAX ? -1 : i;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // merge + exact refine + certification: one wave per query
 // ---------------------------------------------------------------------------
 template <int DT>
@@ -749,7 +1087,48 @@ static hipError_t scan_t(const ScanParams& p, hipStream_t s) {
     return hipGetLastError();
 }
 
+template <int DT, int METRIC, int KSTEPS>
+static hipError_t scan_v2_t(const ScanParams& p, hipStream_t s) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_scan_qreg<DT, METRIC, KSTEPS>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, V2_LDS_BYTES);
+    if (e != hipSuccess) return e;
+    const int grid = p.qt_per_xcd > 0 ? 8 * p.qt_per_xcd * p.splits : p.n_qtiles * p.splits;
+    hipLaunchKernelGGL((k_scan_qreg<DT, METRIC, KSTEPS>), dim3(grid), dim3(SCAN_THREADS), V2_LDS_BYTES, s, p);
+    return hipGetLastError();
+}
+
+template <int DT, int METRIC>
+static hipError_t scan_v2_dispatch(const ScanParams& p, hipStream_t s, bool* handled) {
+    *handled = true;
+    switch (p.row_bytes / 64) {
+        case 8: return scan_v2_t<DT, METRIC, 8>(p, s);
+        case 12: return scan_v2_t<DT, METRIC, 12>(p, s);
+        case 16: return scan_v2_t<DT, METRIC, 16>(p, s);
+        case 24: return scan_v2_t<DT, METRIC, 24>(p, s);
+        default: *handled = false; return hipSuccess;
+    }
+}
+
+bool scan_v2_supported(int row_bytes) {
+    const int ks = row_bytes / 64;
+    return ks == 8 || ks == 12 || ks == 16 || ks == 24;
+}
+
 hipError_t launch_scan(int st_dt, int metric, const ScanParams& p, hipStream_t s) {
+    if (scan_v2_supported(p.row_bytes) && !getenv("FX_SCAN_V1")) {
+        bool handled = false;
+        hipError_t e;
+        if (metric == L2) {
+            if (st_dt == F32) e = scan_v2_dispatch<F32, L2>(p, s, &handled);
+            else if (st_dt == BF16) e = scan_v2_dispatch<BF16, L2>(p, s, &handled);
+            else e = scan_v2_dispatch<F16, L2>(p, s, &handled);
+        } else {
+            if (st_dt == F32) e = scan_v2_dispatch<F32, IP>(p, s, &handled);
+            else if (st_dt == BF16) e = scan_v2_dispatch<BF16, IP>(p, s, &handled);
+            else e = scan_v2_dispatch<F16, IP>(p, s, &handled);
+        }
+        if (handled) return e;
+    }
     if (metric == L2) {
         if (st_dt == F32) return scan_t<F32, L2>(p, s);
         if (st_dt == BF16) return scan_t<BF16, L2>(p, s);

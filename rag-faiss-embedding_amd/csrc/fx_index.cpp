@@ -8,9 +8,11 @@
 #include <float.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -90,7 +92,7 @@ struct FxIndex {
     hipStream_t own_stream = nullptr;
     hipStream_t user_stream = nullptr;
     // search workspace
-    DevBuf qin, qf32, qop, qeps, cand_d, cand_i, dws, iws, flag, fbc_d, fbc_i, stage;
+    DevBuf qin, qf32, qop, qeps, cand_d, cand_i, dws, iws, flag, fbc_d, fbc_i, stage, gtau;
     int64_t last_fallbacks = 0;
     // profiling
     bool profile = false;
@@ -147,11 +149,21 @@ void plan_scan(const FxIndex* h, int64_t nq, ScanParams& p) {
     p.n_ctiles = (int)((h->ntotal + TILE_R - 1) / TILE_R);
     p.qt_per_xcd = p.n_qtiles >= 8 ? (p.n_qtiles + 7) / 8 : 0;
     const int eff_q = p.qt_per_xcd > 0 ? 8 * p.qt_per_xcd : p.n_qtiles;
-    int splits = (1024 + eff_q - 1) / eff_q;
-    // at least ~4 tiles per split so the per-split warm-up stays amortised
-    splits = std::min(splits, std::max(1, p.n_ctiles / 4));
-    splits = std::max(1, std::min(splits, p.n_ctiles));
-    p.splits = splits;
+    // One resident workgroup per CU (150 KiB LDS): pick the split count whose
+    // live workgroups (invalid query tiles exit at once) fill whole rounds of
+    // 256 CUs best, with >= ~4 rounds and >= 4 tiles per split.
+    const int max_splits = std::max(1, p.n_ctiles / 4);
+    const int s0 = std::max(1, std::min(max_splits, (1024 + eff_q - 1) / eff_q));
+    int best = s0;
+    double best_eff = 0.0;
+    for (int s = s0; s <= std::min(max_splits, 4 * s0); ++s) {
+        const double live = (double)p.n_qtiles * s;
+        const double rounds = std::ceil(live / 256.0);
+        const double eff = live / (rounds * 256.0);
+        if (eff > best_eff + 1e-9) { best_eff = eff; best = s; }
+        if (eff > 0.985) break;
+    }
+    p.splits = best;
 }
 
 int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int k, float* D, int64_t* I,
@@ -184,6 +196,10 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
     sp.row_bytes = h->row_bytes;
     sp.qop = qop ? (const char*)qop : (const char*)h->qf32.p;
     sp.nq = nq;
+    sp.dbg = getenv("FX_SCAN_DBG") ? atoi(getenv("FX_SCAN_DBG")) : 0;
+    HIP_TRY(h->gtau.ensure((size_t)sp.n_qtiles * TILE_Q * 4));
+    sp.gtau = (unsigned*)h->gtau.p;
+    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)sp.gtau, 0xff800000u, (size_t)sp.n_qtiles * TILE_Q, s));  // ord(+inf)
     const size_t ncand = (size_t)sp.n_qtiles * sp.splits * TILE_Q * KP;
     HIP_TRY(h->cand_d.ensure(ncand * 4));
     HIP_TRY(h->cand_i.ensure(ncand * 4));
@@ -242,7 +258,7 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
     HIP_TRY(hipMemcpyAsync(&nf, n_flag, 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     h->last_fallbacks = nf;
-    if (nf > 0) {
+    if (nf > 0 && sp.dbg == 0) {
         const int fb_splits = (int)std::max<int64_t>(1, std::min<int64_t>(256, (h->ntotal + 4095) / 4096));
         const int chunk = 64;
         for (int f0 = 0; f0 < nf; f0 += chunk) {
@@ -324,7 +340,7 @@ void fx_index_free(FxIndex* h) {
         if (h->norms) (void)hipFree(h->norms);
         if (h->max_sq_bits) (void)hipFree(h->max_sq_bits);
         for (DevBuf* b : {&h->qin, &h->qf32, &h->qop, &h->qeps, &h->cand_d, &h->cand_i, &h->dws, &h->iws, &h->flag,
-                          &h->fbc_d, &h->fbc_i, &h->stage})
+                          &h->fbc_d, &h->fbc_i, &h->stage, &h->gtau})
             b->release();
         for (auto& pr : h->ev_scan) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
         for (auto& pr : h->ev_merge) (void)hipEventDestroy(pr.second);

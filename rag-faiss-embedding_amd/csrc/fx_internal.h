@@ -44,6 +44,9 @@ struct ScanParams {
     int qt_per_xcd;        // query tiles assigned per XCD group
     float* cand_d;         // [n_qtiles][splits][TILE_Q][KP]
     int* cand_i;
+    int dbg;               // ablation switches (FX_SCAN_DBG; 0 in production)
+    unsigned* gtau;        // [n_qtiles * TILE_Q] order-preserving bits of the best
+                           // known KP-th key per query across splits (atomicMin)
 };
 
 struct RefineParams {

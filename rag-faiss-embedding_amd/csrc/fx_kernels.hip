@@ -255,15 +255,29 @@ __device__ __forceinline__ void map_block(int b, const ScanParams& p, int& qtile
     }
 }
 
+// order-preserving float <-> uint (atomicMin on floats of either sign)
+__device__ __forceinline__ unsigned f2ord(float f) {
+    const unsigned u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float ord2f(unsigned o) {
+    return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
+}
+
 // Compact every full list (cnt >= CAP) to its KP best entries; tau = KP-th.
-__device__ __forceinline__ void compact_full(float* lst_d, int* lst_i, int* cnt, float* tau, int wave, int lane) {
+__device__ __forceinline__ void compact_full(float* lst_d, int* lst_i, int* cnt, float* tau, int wave, int lane,
+                                             unsigned* gtau = nullptr) {
     for (int q = wave; q < TILE_Q; q += 4) {
         if (cnt[q] >= CAP) {
             float d = lst_d[q * CAP + lane];
             int i = lst_i[q * CAP + lane];
             sort64(d, i, lane);
             if (lane < KP) { lst_d[q * CAP + lane] = d; lst_i[q * CAP + lane] = i; }
-            if (lane == KP - 1) tau[q] = d;
+            if (lane == KP - 1) {
+                tau[q] = d;
+                // publish: no split needs keys above the best KP-th of any split
+                if (gtau) atomicMin(gtau + q, f2ord(d));
+            }
             if (lane == 0) cnt[q] = KP;
         }
     }
@@ -478,20 +492,20 @@ template <> struct AsmMma<BF16> {
     typedef bf16x8 A;
     typedef bf16x8 B;
     static __device__ __forceinline__ void mma(f32x4& c, const A& a, const B& b) {
-        asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "a"(b));
+        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "a"(b));
     }
     static __device__ __forceinline__ void mma0(f32x4& c, const A& a, const B& b) {
-        asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=v"(c) : "v"(a), "a"(b));
+        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(c) : "v"(a), "a"(b));
     }
 };
 template <> struct AsmMma<F16> {
     typedef f16x8 A;
     typedef f16x8 B;
     static __device__ __forceinline__ void mma(f32x4& c, const A& a, const B& b) {
-        asm("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "a"(b));
+        asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "a"(b));
     }
     static __device__ __forceinline__ void mma0(f32x4& c, const A& a, const B& b) {
-        asm("v_mfma_f32_16x16x32_f16 %0, %1, %2, 0" : "=v"(c) : "v"(a), "a"(b));
+        asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, 0" : "=a"(c) : "v"(a), "a"(b));
     }
 };
 // f32: a 64-B k-chunk is 4 k-steps of 16x16x4 (see Frag<F32>); B is kept as 4
@@ -501,16 +515,16 @@ template <> struct AsmMma<F32> {
     typedef f32x4 A;
     typedef Bf32 B;
     static __device__ __forceinline__ void mma(f32x4& c, const A& a, const B& b) {
-        asm("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(c) : "v"(a[0]), "a"(b.x[0]));
-        asm("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(c) : "v"(a[1]), "a"(b.x[1]));
-        asm("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(c) : "v"(a[2]), "a"(b.x[2]));
-        asm("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(c) : "v"(a[3]), "a"(b.x[3]));
+        asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+a"(c) : "v"(a[0]), "a"(b.x[0]));
+        asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+a"(c) : "v"(a[1]), "a"(b.x[1]));
+        asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+a"(c) : "v"(a[2]), "a"(b.x[2]));
+        asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+a"(c) : "v"(a[3]), "a"(b.x[3]));
     }
     static __device__ __forceinline__ void mma0(f32x4& c, const A& a, const B& b) {
-        asm("v_mfma_f32_16x16x4_f32 %0, %1, %2, 0" : "=v"(c) : "v"(a[0]), "a"(b.x[0]));
-        asm("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(c) : "v"(a[1]), "a"(b.x[1]));
-        asm("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(c) : "v"(a[2]), "a"(b.x[2]));
-        asm("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(c) : "v"(a[3]), "a"(b.x[3]));
+        asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, 0" : "=a"(c) : "v"(a[0]), "a"(b.x[0]));
+        asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+a"(c) : "v"(a[1]), "a"(b.x[1]));
+        asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+a"(c) : "v"(a[2]), "a"(b.x[2]));
+        asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+a"(c) : "v"(a[3]), "a"(b.x[3]));
     }
 };
 
@@ -523,23 +537,28 @@ __device__ __forceinline__ uint32_t lds_off(const void* p) {
 // would otherwise treat them as possibly aliasing the in-flight LDS-DMA ring and
 // drain it with s_waitcnt vmcnt(0) once per tile.  Their data is ordered by the
 // stage's counted vmcnt + barrier (norms) or by the previous barrier (tau, flag).
-__device__ __forceinline__ void lds_read_epi(const float* norm_base, const float* tau_base, f32x4 (&y)[8],
-                                             float (&t)[2]) {
+// norm_base -> row rl0 of the tile's slot ([wave][32 norms | 32 gtau], 256 B
+// per wave: row r lives at (r/32)*256 + (r%32)*4); gt_base -> this lane's
+// query in the wave's gtau half.
+__device__ __forceinline__ void lds_read_epi(const char* norm_base, const float* tau_base, const char* gt_base,
+                                             f32x4 (&y)[8], float (&t)[2], unsigned (&gt)[2]) {
     asm volatile(
-        "ds_read_b128 %0, %10\n\t"
-        "ds_read_b128 %1, %10 offset:64\n\t"
-        "ds_read_b128 %2, %10 offset:128\n\t"
-        "ds_read_b128 %3, %10 offset:192\n\t"
-        "ds_read_b128 %4, %10 offset:256\n\t"
-        "ds_read_b128 %5, %10 offset:320\n\t"
-        "ds_read_b128 %6, %10 offset:384\n\t"
-        "ds_read_b128 %7, %10 offset:448\n\t"
-        "ds_read_b32 %8, %11\n\t"
-        "ds_read_b32 %9, %11 offset:64\n\t"
+        "ds_read_b128 %0, %12\n\t"
+        "ds_read_b128 %1, %12 offset:64\n\t"
+        "ds_read_b128 %2, %12 offset:256\n\t"
+        "ds_read_b128 %3, %12 offset:320\n\t"
+        "ds_read_b128 %4, %12 offset:512\n\t"
+        "ds_read_b128 %5, %12 offset:576\n\t"
+        "ds_read_b128 %6, %12 offset:768\n\t"
+        "ds_read_b128 %7, %12 offset:832\n\t"
+        "ds_read_b32 %8, %13\n\t"
+        "ds_read_b32 %9, %13 offset:64\n\t"
+        "ds_read_b32 %10, %14\n\t"
+        "ds_read_b32 %11, %14 offset:64\n\t"
         "s_waitcnt lgkmcnt(0)"
         : "=&v"(y[0]), "=&v"(y[1]), "=&v"(y[2]), "=&v"(y[3]), "=&v"(y[4]), "=&v"(y[5]), "=&v"(y[6]), "=&v"(y[7]),
-          "=&v"(t[0]), "=&v"(t[1])
-        : "v"(lds_off(norm_base)), "v"(lds_off(tau_base))
+          "=&v"(t[0]), "=&v"(t[1]), "=&v"(gt[0]), "=&v"(gt[1])
+        : "v"(lds_off(norm_base)), "v"(lds_off(tau_base)), "v"(lds_off(gt_base))
         : "memory");
 }
 __device__ __forceinline__ int lds_read_flag(const volatile int* f) {
@@ -552,16 +571,17 @@ template <int M>
 __device__ __forceinline__ void acc_fence(f32x4 (&acc)[M][2]) {
     static_assert(M == 8, "acc_fence operand list is written for 8x2 accumulators");
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7"
-                 : "+v"(acc[0][0]), "+v"(acc[0][1]), "+v"(acc[1][0]), "+v"(acc[1][1]), "+v"(acc[2][0]),
-                   "+v"(acc[2][1]), "+v"(acc[3][0]), "+v"(acc[3][1]), "+v"(acc[4][0]), "+v"(acc[4][1]),
-                   "+v"(acc[5][0]), "+v"(acc[5][1]), "+v"(acc[6][0]), "+v"(acc[6][1]), "+v"(acc[7][0]),
-                   "+v"(acc[7][1]));
+                 : "+a"(acc[0][0]), "+a"(acc[0][1]), "+a"(acc[1][0]), "+a"(acc[1][1]), "+a"(acc[2][0]),
+                   "+a"(acc[2][1]), "+a"(acc[3][0]), "+a"(acc[3][1]), "+a"(acc[4][0]), "+a"(acc[4][1]),
+                   "+a"(acc[5][0]), "+a"(acc[5][1]), "+a"(acc[6][0]), "+a"(acc[6][1]), "+a"(acc[7][0]),
+                   "+a"(acc[7][1]));
 }
 
 constexpr int V2_NS = 5;
 constexpr int V2_STAGE = TILE_R * STAGE_B;                     // 16 KiB
-constexpr int V2_NORM_OFF = V2_NS * V2_STAGE;                  // 4 slots x 512 B
-constexpr int V2_LD_OFF = V2_NORM_OFF + 4 * TILE_R * 4;
+constexpr int V2_NORM_OFF = V2_NS * V2_STAGE;                  // 4 slots x 4 waves x 256 B
+constexpr int V2_SLOT_B = 4 * 256;                              // [wave][32 norms | 32 gtau]
+constexpr int V2_LD_OFF = V2_NORM_OFF + 4 * V2_SLOT_B;
 constexpr int V2_LI_OFF = V2_LD_OFF + TILE_Q * CAP * 4;
 constexpr int V2_CNT_OFF = V2_LI_OFF + TILE_Q * CAP * 4;
 constexpr int V2_TAU_OFF = V2_CNT_OFF + TILE_Q * 4;
@@ -642,7 +662,9 @@ __device__ __forceinline__ bool epi_retry(const f32x4 (&acc)[M][N], const float 
     return ovf;
 }
 
-template <int DT, int METRIC, int KSTEPS>
+// ABL: compile-time ablation switches for profiling builds only (0 = product):
+// 2 = no corpus DMA, 4 = no MFMA, 8 = no epilogue
+template <int DT, int METRIC, int KSTEPS, int ABL = 0>
 __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_qreg(ScanParams p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     typedef typename AsmMma<DT>::A frag_t;
@@ -685,16 +707,25 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_qreg(ScanParams p) {
         const int bi = wave * 4 + jj, rblk = bi >> 1, kb = bi & 1;
         offs[jj] = (rblk * 16 + (lane & 15)) * rb + kb * 64 + (lane >> 4) * 16;
     }
+    const unsigned* gtq = p.gtau + q0 + wave * 32;
     auto issue = [&](int g) {
         int t = g / SPT;
         const int j = g - t * SPT;
         if (t >= ntiles) t = ntiles - 1;  // dummy stage: uniform vmcnt accounting
-        const int64_t row0 = (int64_t)(ct0 + t) * TILE_R;
+        int64_t row0 = (int64_t)(ct0 + t) * TILE_R;
+        if (p.dbg & 1) row0 = (int64_t)(ct0 + (t & 7)) * TILE_R;  // ablation: L2-resident corpus
         char* slot = smem + (g % NS) * V2_STAGE;
         const char* src = p.codes + row0 * rb + j * STAGE_B;
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) glds16(src + offs[jj], slot + (wave * 4 + jj) * 1024);
-        if (lane < 8) glds16(p.norms + row0 + wave * 32 + lane * 4, smem + V2_NORM_OFF + (t & 3) * 512 + wave * 128);
+        // lanes 0-7: this wave's 32 row norms of the tile; lanes 8-15: the
+        // shared thresholds of this wave's 32 queries (refreshed every stage;
+        // any version is a valid bound)
+        if (lane < 16) {
+            const void* src = lane < 8 ? (const void*)(p.norms + row0 + wave * 32 + lane * 4)
+                                       : (const void*)(gtq + (lane - 8) * 4);
+            glds16(src, smem + V2_NORM_OFF + (t & 3) * V2_SLOT_B + wave * 256);
+        }
     };
 
 #pragma unroll
@@ -710,18 +741,19 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_qreg(ScanParams p) {
 
     // slow path: compact full lists and re-push pending survivors of tile `tp`
     auto overflow = [&](int tp) {
-        const float* nb = (const float*)(smem + V2_NORM_OFF + (tp & 3) * 512);
+        const char* nb = smem + V2_NORM_OFF + (tp & 3) * V2_SLOT_B;
         float yn[M][4];
 #pragma unroll
         for (int m = 0; m < M; ++m) {
-            const float4 v = *(const float4*)(nb + rl0 + m * 16);
+            const int r = rl0 + m * 16;
+            const float4 v = *(const float4*)(nb + (r >> 5) * 256 + (r & 31) * 4);
             yn[m][0] = v.x; yn[m][1] = v.y; yn[m][2] = v.z; yn[m][3] = v.w;
         }
         const int trow0 = (ct0 + tp) * TILE_R;
         while (*flag) {
             __syncthreads();
             if (tid == 0) *flag = 0;
-            compact_full(lst_d, lst_i, cnt, tau, wave, lane);
+            compact_full(lst_d, lst_i, cnt, tau, wave, lane, p.gtau + q0);
             __syncthreads();
             float tn[N];
 #pragma unroll
@@ -731,36 +763,59 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_qreg(ScanParams p) {
         }
     };
 
+    // ring reads are issued one stage ahead into a second register set (aA /
+    // aB by stage parity); stage g's MFMAs then overlap stage g+1's ds_reads.
+    frag_t aA[2][M], aB[2][M];
+    auto read_stage = [&](int g, frag_t (&a)[2][M]) {
+        const char* slot = smem + (g % NS) * V2_STAGE;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int m = 0; m < M; ++m) a[kb][m] = *(const frag_t*)(slot + (m * 2 + kb) * 1024 + lane * 16);
+    };
+    const int G = ntiles * SPT;
+    // stage 0 landed (own DMA: vmcnt leaves stages 1..NS-2 in flight) + barrier
+    asm volatile("s_waitcnt vmcnt(15)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (G > 0) read_stage(0, aA);
+
     for (int t = 0; t < ntiles; ++t) {
         // K loop of one 128-row tile, fully unrolled (B fragments are indexed
         // by k-step: must be compile-time to stay in registers)
 #pragma unroll
         for (int j = 0; j < SPT; ++j) {
             const int g = t * SPT + j;
-            asm volatile("s_waitcnt vmcnt(15) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            issue(g + NS - 1);
-            const char* slot = smem + (g % NS) * V2_STAGE;
+            frag_t (&cur)[2][M] = (j & 1) ? aB : aA;
+            frag_t (&nxt)[2][M] = (j & 1) ? aA : aB;
+            // stage g+1 landed for every wave; every wave is done with the
+            // slot the next DMA overwrites ((g-1) % NS, read two stages ago)
+            asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            // (a tile's last stage defers the prefetch past the epilogue, which
+            // needs the registers)
+            if (j + 1 < SPT) read_stage(g + 1, nxt);
+            if (!(ABL & 2)) issue(g + NS - 1);
+            if (!(ABL & 4))
 #pragma unroll
-            for (int kb = 0; kb < 2; ++kb) {
-                frag_t a[M];
-#pragma unroll
-                for (int m = 0; m < M; ++m) a[m] = *(const frag_t*)(slot + (m * 2 + kb) * 1024 + lane * 16);
+            for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
                 for (int m = 0; m < M; ++m)
 #pragma unroll
                     for (int n = 0; n < N; ++n) {
-                        if (j == 0 && kb == 0) AsmMma<DT>::mma0(acc[m][n], a[m], b[0][n]);
-                        else AsmMma<DT>::mma(acc[m][n], a[m], b[2 * j + kb][n]);
+                        if (j == 0 && kb == 0) AsmMma<DT>::mma0(acc[m][n], cur[kb][m], b[0][n]);
+                        else AsmMma<DT>::mma(acc[m][n], cur[kb][m], b[2 * j + kb][n]);
                     }
-            }
         }
         // epilogue: filter against tau, push survivors into the LDS lists
         acc_fence<M>(acc);
-        {
-            const float* nb = (const float*)(smem + V2_NORM_OFF + (t & 3) * 512);
+        if (!(ABL & 8)) {
+            const char* nb = smem + V2_NORM_OFF + (t & 3) * V2_SLOT_B;
             f32x4 y4[M];
             float tn[N];
-            lds_read_epi(nb + rl0, tau + qloc[0], y4, tn);
+            unsigned gt[N];
+            lds_read_epi(nb + rl0 * 4, tau + qloc[0], nb + wave * 256 + 128 + (lane & 15) * 4, y4, tn, gt);
+            tn[0] = fminf(tn[0], ord2f(gt[0]));
+            tn[1] = fminf(tn[1], ord2f(gt[1]));
             float yn[M][4];
 #pragma unroll
             for (int m = 0; m < M; ++m) {
@@ -773,7 +828,9 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_qreg(ScanParams p) {
             if (epi_push<M, N, METRIC>(acc, yn, qloc, tn, rl0, rlim, trow0, pend, lst_d, lst_i, cnt)) *flag = 1;
         }
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
         if (lds_read_flag(flag)) overflow(t);
+        if (t + 1 < ntiles) read_stage((t + 1) * SPT, aA);  // SPT is even: tile starts in aA
     }
     // final flush: sorted top-KP per query of this (query tile, split)
     __syncthreads();
@@ -1097,9 +1154,31 @@ static hipError_t scan_v2_t(const ScanParams& p, hipStream_t s) {
     return hipGetLastError();
 }
 
+template <int DT, int METRIC, int KSTEPS, int ABL>
+static hipError_t scan_abl_t(const ScanParams& p, hipStream_t s) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_scan_qreg<DT, METRIC, KSTEPS, ABL>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, V2_LDS_BYTES);
+    if (e != hipSuccess) return e;
+    const int grid = p.qt_per_xcd > 0 ? 8 * p.qt_per_xcd * p.splits : p.n_qtiles * p.splits;
+    hipLaunchKernelGGL((k_scan_qreg<DT, METRIC, KSTEPS, ABL>), dim3(grid), dim3(SCAN_THREADS), V2_LDS_BYTES, s, p);
+    return hipGetLastError();
+}
+
 template <int DT, int METRIC>
 static hipError_t scan_v2_dispatch(const ScanParams& p, hipStream_t s, bool* handled) {
     *handled = true;
+#ifdef FX_ABLATION
+    if (DT == BF16 && METRIC == L2 && p.row_bytes == 1536 && p.dbg >= 2) {
+        switch (p.dbg) {
+            case 2: return scan_abl_t<DT, METRIC, 24, 2>(p, s);
+            case 4: return scan_abl_t<DT, METRIC, 24, 4>(p, s);
+            case 8: return scan_abl_t<DT, METRIC, 24, 8>(p, s);
+            case 6: return scan_abl_t<DT, METRIC, 24, 6>(p, s);
+            case 14: return scan_abl_t<DT, METRIC, 24, 14>(p, s);
+            default: break;
+        }
+    }
+#endif
     switch (p.row_bytes / 64) {
         case 8: return scan_v2_t<DT, METRIC, 8>(p, s);
         case 12: return scan_v2_t<DT, METRIC, 12>(p, s);

@@ -36,6 +36,7 @@ import torch.distributed as dist  # noqa: E402
 
 import amd_fx  # noqa: E402,F401
 from rag_faiss_embedding_amd import faiss as fx  # noqa: E402
+from rag_faiss_embedding_amd.sharded import ShardedIndexFlatL2, shard_bounds  # noqa: E402
 
 METRIC = "queries/sec + recall@10 vs CPU FAISS, 10M×768 flat index, 1/2/4/8 MI355X"
 CORPUS_SEED, QUERY_SEED = 1234, 4321
@@ -58,8 +59,7 @@ def log(*a):
 
 
 def build_shard(ix, rank, world, n_total, d, dtype, device):
-    lo = n_total * rank // world
-    hi = n_total * (rank + 1) // world
+    lo, hi = shard_bounds(n_total, world, rank)
     ix.reserve(hi - lo)
     chunk = 1 << 20
     buf = torch.empty((min(chunk, hi - lo), d), dtype=TORCH_DT[dtype], device=device)
@@ -73,14 +73,10 @@ def build_shard(ix, rank, world, n_total, d, dtype, device):
     return lo, hi
 
 
-def one_step(ix, xq, k, world, gath):
-    D, I = ix.search(xq, k)
-    if world == 1:
-        return D, I
-    Dg, Ig = gath
-    dist.all_gather_into_tensor(Dg.view(-1, k), D)
-    dist.all_gather_into_tensor(Ig.view(-1, k), I)
-    return fx.merge_shards(ix.metric_type, Dg, Ig, k)
+def one_step(six, xq, k):
+    # ShardedIndexFlatL2.search: local fused scan -> RCCL all_gather of the
+    # (nq x k) lists -> on-device merge (world 1: local scan only)
+    return six.search(xq, k)
 
 
 def oracle_lib_native():
@@ -121,10 +117,16 @@ def cpu_baseline_and_recall(args, n_total, d, k, D, I, nthreads):
     res["recall_sample"] = f"{nr} queries x full {n_total}-row corpus, exact CPU oracle ({t_rec:.1f}s)"
     # timed baseline: BLAS-path port on a corpus slice, extrapolated to n_total
     rows = min(n_total, args.cpu_rows)
-    nq_s = args.cpu_queries
     xb = C.synth(CORPUS_SEED, 0, rows, d, nthreads)
+    # size the timed sample to ~args.cpu_seconds of CPU work (calibrated)
+    xcal = C.synth(QUERY_SEED, 0, 128, d, nthreads)
+    t0 = time.time()
+    C.knn_blas(xcal, xb, k, nthreads, lib=lib)
+    tcal = max(time.time() - t0, 1e-3)
+    nq_s = int(min(50_000, max(128, 128 * args.cpu_seconds / tcal)))
+    if args.cpu_queries:
+        nq_s = args.cpu_queries
     xqs = C.synth(QUERY_SEED, 0, nq_s, d, nthreads)
-    C.knn_blas(xqs[:8], xb[:4096], k, nthreads, lib=lib)  # warm
     t0 = time.time()
     C.knn_blas(xqs, xb, k, nthreads, lib=lib)
     t = time.time() - t0
@@ -163,7 +165,8 @@ def main():
     ap.add_argument("--rows", type=int, default=0, help="override corpus rows (testing)")
     ap.add_argument("--recall-queries", type=int, default=32)
     ap.add_argument("--cpu-rows", type=int, default=1_000_000)
-    ap.add_argument("--cpu-queries", type=int, default=1000)
+    ap.add_argument("--cpu-queries", type=int, default=0, help="fixed CPU sample (0: auto-size)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline sample time")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline / recall leg")
     args = ap.parse_args()
 
@@ -188,22 +191,20 @@ def main():
     n_local = hi - lo
     xq = torch.empty((nq, d), dtype=TORCH_DT[dtype], device=device)
     fx.synth_fill(xq, 0, QUERY_SEED)
-    gath = None
-    if world > 1:
-        gath = (torch.empty((world, nq, k), dtype=torch.float32, device=device),
-                torch.empty((world, nq, k), dtype=torch.int64, device=device))
+    six = ShardedIndexFlatL2(d, n_total, local_index=ix,
+                             merge_fn=lambda Dg, Ig, kk: fx.merge_shards(fx.METRIC_L2, Dg, Ig, kk))
     torch.cuda.synchronize()
     log(f"[rank {rank}] shard rows [{lo}, {hi}) built in {time.time() - t0:.1f}s")
 
     for _ in range(args.warmup):
-        one_step(ix, xq, k, world, gath)
+        one_step(six, xq, k)
     ix.profile(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        D, I = one_step(ix, xq, k, world, gath)
+        D, I = one_step(six, xq, k)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

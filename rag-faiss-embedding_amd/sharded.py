@@ -1,0 +1,93 @@
+"""Row-sharded flat index over the GPUs of one node (one process per GPU).
+
+The reference is single-process; the multi-GPU layout
+is this build's own: the corpus is split into contiguous row blocks, rank r
+holding global rows [offset_r, offset_r + n_r).  A search runs the local
+fused scan on every rank (local top-k with GLOBAL ids), exchanges the
+(nq x k) result lists with ONE all_gather over RCCL/xGMI (the only data-path
+collective), and merges them on the device (``fx_merge_shards``).  Because the
+offsets are monotone in rank, "ties -> smaller id" survives the merge.
+
+Works with any ``torch.distributed`` process group: ``nccl`` (= RCCL) with
+device tensors in production, ``gloo`` with host tensors in the CPU tests,
+where ``local_index`` / ``merge_fn`` can be test doubles.
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def shard_bounds(n_total: int, world: int, rank: int) -> Tuple[int, int]:
+    """Contiguous, near-equal row block of ``rank`` (same rule as bench.py)."""
+    return n_total * rank // world, n_total * (rank + 1) // world
+
+
+class ShardedIndexFlatL2:
+    """``IndexFlatL2`` semantics over a process group.
+
+    add(x_global_block, row0): every rank is handed a block of global rows
+    starting at ``row0`` (the same block on every rank, or only its own part)
+    and keeps the rows it owns; ``n_total`` fixes the ownership split.
+    """
+
+    def __init__(self, d: int, n_total: int, dtype: str = "float32", group=None, device: Optional[int] = None,
+                 local_index=None, merge_fn: Optional[Callable] = None):
+        self.d = int(d)
+        self.n_total = int(n_total)
+        self.group = group
+        ready = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(group) if ready else 1
+        self.rank = dist.get_rank(group) if ready else 0
+        self.lo, self.hi = shard_bounds(self.n_total, self.world, self.rank)
+        if local_index is None:
+            from . import faiss as fx
+            local_index = fx.IndexFlatL2(d, dtype=dtype, device=device if device is not None else 0)
+            local_index.set_id_offset(self.lo)
+            self._merge = lambda Dg, Ig, k: fx.merge_shards(fx.METRIC_L2, Dg, Ig, k)
+        else:
+            self._merge = merge_fn
+        if merge_fn is not None:
+            self._merge = merge_fn
+        self.local = local_index
+
+    @property
+    def ntotal(self) -> int:
+        if self.world == 1:
+            return self.local.ntotal
+        t = torch.tensor([self.local.ntotal], dtype=torch.int64)
+        if dist.get_backend(self.group) == "nccl":
+            t = t.cuda()
+        dist.all_reduce(t, group=self.group)
+        return int(t.item())
+
+    def add(self, x, row0: int = 0) -> None:
+        """Keep the rows of ``x`` (global rows row0 .. row0+len(x)-1) that
+        fall in this rank's block."""
+        n = x.shape[0]
+        a = max(self.lo, row0)
+        b = min(self.hi, row0 + n)
+        if b > a:
+            self.local.add(x[a - row0:b - row0])
+
+    def search(self, xq, k: int):
+        """Global top-k: local scan -> all_gather of (D, I) -> merge."""
+        D, I = self.local.search(xq, k)
+        if self.world == 1:
+            return D, I
+        is_np = isinstance(D, np.ndarray)
+        Dt = torch.from_numpy(D) if is_np else D
+        It = torch.from_numpy(I) if is_np else I
+        Dl = [torch.empty_like(Dt) for _ in range(self.world)]
+        Il = [torch.empty_like(It) for _ in range(self.world)]
+        dist.all_gather(Dl, Dt.contiguous(), group=self.group)
+        dist.all_gather(Il, It.contiguous(), group=self.group)
+        Dg = torch.stack(Dl)
+        Ig = torch.stack(Il)
+        Dm, Im = self._merge(Dg, Ig, k)
+        if is_np:
+            return np.asarray(Dm), np.asarray(Im)
+        return Dm, Im

@@ -166,7 +166,7 @@ def main():
     ap.add_argument("--recall-queries", type=int, default=32)
     ap.add_argument("--cpu-rows", type=int, default=1_000_000)
     ap.add_argument("--cpu-queries", type=int, default=0, help="fixed CPU sample (0: auto-size)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline sample time")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="target CPU baseline sample time")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline / recall leg")
     args = ap.parse_args()
 
@@ -238,7 +238,7 @@ def main():
         roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(gbs / HBM_PEAK_GBS, 4)}
     roof["traffic"] = read_pmc_traffic(args.config, n_local, nq)
-    roof["kernel"] = "k_scan_topk (fused MFMA distance GEMM + top-k)"
+    roof["kernel"] = "k_scan_qreg (fused MFMA distance GEMM + top-k select)"
     roof["kernel_ms_avg"] = round(scan_avg_ms, 4)
     roof["launches"] = launches
     roof["merge_refine_ms_avg"] = round(merge_ms / max(launches, 1), 4)

@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""Turn a tools/profile_scan.sh output directory into committed evidence:
+
+  profiles/<round>_<tag>_kernel_stats.csv   rocprofv3 --stats summary (verbatim)
+  profiles/<round>_<tag>_summary.json       per-kernel averages + PMC per launch
+  profiles/pmc_scan_<tag>.json              HBM bytes per scan launch (read by
+                                            bench.py for roofline.traffic)
+
+HBM bytes follow MI355X_MICROARCH.md "HBM": FETCH_SIZE / WRITE_SIZE are KiB;
+on gfx950 FETCH_SIZE reports half the bytes of a wide coalesced stream, so it
+is doubled; Infinity-Cache (MALL) hits are counted in it, not excluded.
+usage: tools/summarize_profile.py <prof_dir> <tag> <round> <rows_per_gpu> <nq>
+"""
+import csv
+import json
+import shutil
+import statistics
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+SCAN = "k_scan_qreg"
+
+
+def counters(path):
+    agg = defaultdict(lambda: defaultdict(list))
+    if not path.exists():
+        return agg
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            agg[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return agg
+
+
+def main():
+    prof, tag, rnd, rows, nq = Path(sys.argv[1]), sys.argv[2], sys.argv[3], int(sys.argv[4]), int(sys.argv[5])
+    out = ROOT / "profiles"
+    out.mkdir(exist_ok=True)
+    stats = prof / "trace" / "run_kernel_stats.csv"
+    shutil.copy(stats, out / f"{rnd}_{tag}_kernel_stats.csv")
+    kern = {}
+    with open(stats) as f:
+        for r in csv.DictReader(f):
+            kern[r["Name"]] = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6,
+                               "pct": float(r["Percentage"])}
+    pmc = {}
+    for sub in ("fetch", "write", "tcc", "sq"):
+        for name, cs in counters(prof / sub / "run_counter_collection.csv").items():
+            if SCAN in name:
+                for c, vals in cs.items():
+                    pmc[c] = statistics.median(vals)
+    scan_name = next(n for n in kern if SCAN in n)
+    res = {"kernels": kern, "scan_kernel": scan_name, "scan_pmc_median_per_launch": pmc,
+           "rows_per_gpu": rows, "nq": nq}
+    if "FETCH_SIZE" in pmc:
+        fetch = pmc["FETCH_SIZE"] * 1024 * 2          # gfx950: FETCH_SIZE = 1/2 of streamed bytes
+        write = pmc.get("WRITE_SIZE", 0.0) * 1024
+        res["hbm_bytes_per_launch"] = fetch + write
+        res["hbm_note"] = ("(2*FETCH_SIZE + WRITE_SIZE) KiB -> bytes; includes Infinity-Cache hits "
+                           "(MI355X_MICROARCH.md HBM section)")
+    if "TCC_HIT_sum" in pmc:
+        res["l2_hit_rate"] = pmc["TCC_HIT_sum"] / (pmc["TCC_HIT_sum"] + pmc["TCC_MISS_sum"])
+    if "SQ_VALU_MFMA_BUSY_CYCLES" in pmc and "GRBM_GUI_ACTIVE" in pmc:
+        # GRBM_GUI_ACTIVE sums the 8 XCDs; MFMA busy cycles sum the 1024 SIMDs
+        per_xcd = pmc["GRBM_GUI_ACTIVE"] / 8
+        res["mfma_busy_frac"] = pmc["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024 / per_xcd
+        res["effective_clock_ghz"] = per_xcd / (kern[scan_name]["avg_ms"] * 1e6)
+    if "SQ_WAIT_ANY" in pmc:
+        res["wave_wait_frac"] = pmc["SQ_WAIT_ANY"] / pmc["SQ_WAVE_CYCLES"]
+    (out / f"{rnd}_{tag}_summary.json").write_text(json.dumps(res, indent=1))
+    if "hbm_bytes_per_launch" in res:
+        (out / f"pmc_scan_{tag}.json").write_text(json.dumps(
+            {"rows_per_gpu": rows, "nq": nq, "hbm_bytes_per_launch": res["hbm_bytes_per_launch"],
+             "source": f"profiles/{rnd}_{tag}_summary.json"}, indent=1))
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

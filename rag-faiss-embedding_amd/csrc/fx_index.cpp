@@ -179,11 +179,8 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
         qdev = h->qin.p;
     }
     HIP_TRY(h->qf32.ensure((size_t)nq_pad * h->kdim * 4));
-    void* qop = nullptr;
-    if (h->dtype != F32) {
-        HIP_TRY(h->qop.ensure((size_t)nq_pad * h->row_bytes));
-        qop = h->qop.p;
-    }
+    HIP_TRY(h->qop.ensure((size_t)nq_pad * h->row_bytes));
+    void* qop = h->qop.p;
     HIP_TRY(h->qeps.ensure((size_t)nq * 4));
     HIP_TRY(launch_prep_queries(qdev, q_dtype, nq, nq_pad, h->d, h->kdim, h->dtype, h->metric, (float*)h->qf32.p,
                                 qop, (float*)h->qeps.p, sqrt((double)h->max_sq), s));
@@ -194,7 +191,7 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
     sp.norms = h->norms;
     sp.ntotal = h->ntotal;
     sp.row_bytes = h->row_bytes;
-    sp.qop = qop ? (const char*)qop : (const char*)h->qf32.p;
+    sp.qop = (const char*)qop;
     sp.nq = nq;
     sp.dbg = getenv("FX_SCAN_DBG") ? atoi(getenv("FX_SCAN_DBG")) : 0;
     HIP_TRY(h->gtau.ensure((size_t)sp.n_qtiles * TILE_Q * 4));

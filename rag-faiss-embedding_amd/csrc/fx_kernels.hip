@@ -180,10 +180,13 @@ __global__ __launch_bounds__(256) void k_prep_queries(const void* __restrict__ q
     for (int c = lane; c < kdim; c += 64) {
         float v = (live && c < d) ? load_elem(q, r * d + c, q_dt) : 0.0f;
         qf32[r * (int64_t)kdim + c] = v;
-        if (qop) {
-            float st = round_to(v, st_dt);
+        {
+            // scan operand: x rounded to the storage dtype, pre-scaled (exactly,
+            // by a power of two) so that the MFMA accumulator is the key:
+            // L2: acc = -2 x.y (+ |y|^2 from the accumulator init); IP: -x.y
+            const float st = round_to(v, st_dt);
             inexact |= st != v;
-            store_elem(qop, r * (int64_t)kdim + c, st_dt, st);
+            store_elem(qop, r * (int64_t)kdim + c, st_dt, st * (metric == L2 ? -2.0f : -1.0f));
         }
         s += (double)v * (double)v;
     }
@@ -391,7 +394,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_topk(ScanParams p) {
                 for (int m = 0; m < 4; ++m)
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
-                        const float v = METRIC == L2 ? fmaf(-2.0f, acc[m][n][i], yn[m][i]) : -acc[m][n][i];
+                        const float v = METRIC == L2 ? acc[m][n][i] + yn[m][i] : acc[m][n][i];
                         const int rl = rl0 + m * 16 + i;
                         if (qv[n] && rl < rlim && v <= tn[n]) {
                             const int s = atomicAdd(&cnt[qloc[n]], 1);
@@ -422,7 +425,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_topk(ScanParams p) {
                             const unsigned bit = 1u << (m * 4 + i);
                             if (pend[n] & bit) {
                                 const float v =
-                                    METRIC == L2 ? fmaf(-2.0f, acc[m][n][i], yn[m][i]) : -acc[m][n][i];
+                                    METRIC == L2 ? acc[m][n][i] + yn[m][i] : acc[m][n][i];
                                 pend[n] &= ~bit;
                                 if (v <= tn[n]) {
                                     const int s = atomicAdd(&cnt[qloc[n]], 1);
@@ -605,7 +608,7 @@ __device__ __forceinline__ bool epi_push(const f32x4 (&acc)[M][N], const float (
         for (int m = 0; m < M; ++m)
 #pragma unroll
             for (int i = 0; i < 4; ++i)
-                mn = fminf(mn, METRIC == L2 ? fmaf(-2.0f, acc[m][n][i], yn[m][i]) : -acc[m][n][i]);
+                mn = fminf(mn, METRIC == L2 ? acc[m][n][i] + yn[m][i] : acc[m][n][i]);
         any |= mn <= tn[n];
     }
     if (!__any(any)) return false;
@@ -616,7 +619,7 @@ __device__ __forceinline__ bool epi_push(const f32x4 (&acc)[M][N], const float (
         for (int m = 0; m < M; ++m)
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const float v = METRIC == L2 ? fmaf(-2.0f, acc[m][n][i], yn[m][i]) : -acc[m][n][i];
+                const float v = METRIC == L2 ? acc[m][n][i] + yn[m][i] : acc[m][n][i];
                 const int rl = rl0 + m * 16 + i;
                 if (rl < rlim && v <= tn[n]) {
                     const int s = atomicAdd(&cnt[qloc[n]], 1);
@@ -645,7 +648,7 @@ __device__ __forceinline__ bool epi_retry(const f32x4 (&acc)[M][N], const float 
             for (int i = 0; i < 4; ++i) {
                 const unsigned bit = 1u << (m * 4 + i);
                 if (pend[n] & bit) {
-                    const float v = METRIC == L2 ? fmaf(-2.0f, acc[m][n][i], yn[m][i]) : -acc[m][n][i];
+                    const float v = METRIC == L2 ? acc[m][n][i] + yn[m][i] : acc[m][n][i];
                     pend[n] &= ~bit;
                     if (v <= tn[n]) {
                         const int s = atomicAdd(&cnt[qloc[n]], 1);
@@ -832,6 +835,348 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_qreg(ScanParams p) {
         if (lds_read_flag(flag)) overflow(t);
         if (t + 1 < ntiles) read_stage((t + 1) * SPT, aA);  // SPT is even: tile starts in aA
     }
+    // final flush: sorted top-KP per query of this (query tile, split)
+    __syncthreads();
+    const int64_t obase = ((int64_t)qtile * p.splits + split) * TILE_Q;
+    for (int q = wave; q < TILE_Q; q += 4) {
+        if (q0 + q >= p.nq) break;
+        const int c = min(cnt[q], CAP);
+        float d = lane < c ? lst_d[q * CAP + lane] : FX_INF;
+        int i = lane < c ? lst_i[q * CAP + lane] : INT_MAX;
+        sort64(d, i, lane);
+        if (lane < KP) {
+            p.cand_d[(obase + q) * KP + lane] = d;
+            p.cand_i[(obase + q) * KP + lane] = i == INT_MAX ? -1 : i;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// scan kernel v3: v2's structure with (a) the accumulator in VGPRs holding the
+// KEY itself -- queries are pre-scaled by -2 (L2) / -1 (IP) and a tile's first
+// MFMA takes srcC = |y|^2 of its rows (L2) -- so the epilogue is a min3 chain
+// with no accumulator reads and no FMA; (b) a 3-set rotation of A-fragment
+// registers (next stage's half-stage reads overlap this stage's MFMAs);
+// (c) the stage's 5 LDS-DMA pieces interleaved between MFMA groups.
+// ---------------------------------------------------------------------------
+template <int DT> struct AsmMmaV;
+template <> struct AsmMmaV<BF16> {
+    typedef bf16x8 A;
+    typedef bf16x8 B;
+    static __device__ __forceinline__ void mma(f32x4& c, const A& a, const B& b) {
+        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "a"(b));
+    }
+    static __device__ __forceinline__ void mmac(f32x4& c, const A& a, const B& b, const f32x4& c0) {
+        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %3" : "=&v"(c) : "v"(a), "a"(b), "v"(c0));
+    }
+};
+template <> struct AsmMmaV<F16> {
+    typedef f16x8 A;
+    typedef f16x8 B;
+    static __device__ __forceinline__ void mma(f32x4& c, const A& a, const B& b) {
+        asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "a"(b));
+    }
+    static __device__ __forceinline__ void mmac(f32x4& c, const A& a, const B& b, const f32x4& c0) {
+        asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %3" : "=&v"(c) : "v"(a), "a"(b), "v"(c0));
+    }
+};
+template <> struct AsmMmaV<F32> {
+    typedef f32x4 A;
+    typedef Bf32 B;
+    static __device__ __forceinline__ void mma(f32x4& c, const A& a, const B& b) {
+        asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(c) : "v"(a[0]), "a"(b.x[0]));
+        asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(c) : "v"(a[1]), "a"(b.x[1]));
+        asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(c) : "v"(a[2]), "a"(b.x[2]));
+        asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(c) : "v"(a[3]), "a"(b.x[3]));
+    }
+    static __device__ __forceinline__ void mmac(f32x4& c, const A& a, const B& b, const f32x4& c0) {
+        asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %3" : "=&v"(c) : "v"(a[0]), "a"(b.x[0]), "v"(c0));
+        asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(c) : "v"(a[1]), "a"(b.x[1]));
+        asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(c) : "v"(a[2]), "a"(b.x[2]));
+        asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(c) : "v"(a[3]), "a"(b.x[3]));
+    }
+};
+
+__device__ __forceinline__ void acc_fence_v(f32x4 (&acc)[8][2]) {
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7"
+                 : "+v"(acc[0][0]), "+v"(acc[0][1]), "+v"(acc[1][0]), "+v"(acc[1][1]), "+v"(acc[2][0]),
+                   "+v"(acc[2][1]), "+v"(acc[3][0]), "+v"(acc[3][1]), "+v"(acc[4][0]), "+v"(acc[4][1]),
+                   "+v"(acc[5][0]), "+v"(acc[5][1]), "+v"(acc[6][0]), "+v"(acc[6][1]), "+v"(acc[7][0]),
+                   "+v"(acc[7][1]));
+}
+
+// the tile's 8 row-norm quads of this lane (rows rl0 + 16m .. +3), asm so that
+// hipcc does not drain the DMA ring (see lds_read_epi)
+__device__ __forceinline__ void lds_read_norms(const char* base, f32x4 (&y)[8]) {
+    asm volatile(
+        "ds_read_b128 %0, %8\n\t"
+        "ds_read_b128 %1, %8 offset:64\n\t"
+        "ds_read_b128 %2, %8 offset:256\n\t"
+        "ds_read_b128 %3, %8 offset:320\n\t"
+        "ds_read_b128 %4, %8 offset:512\n\t"
+        "ds_read_b128 %5, %8 offset:576\n\t"
+        "ds_read_b128 %6, %8 offset:768\n\t"
+        "ds_read_b128 %7, %8 offset:832\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(y[0]), "=&v"(y[1]), "=&v"(y[2]), "=&v"(y[3]), "=&v"(y[4]), "=&v"(y[5]), "=&v"(y[6]), "=&v"(y[7])
+        : "v"(lds_off(base))
+        : "memory");
+}
+__device__ __forceinline__ void lds_read_tau(const float* tau_base, const char* gt_base, float (&t)[2],
+                                             unsigned (&gt)[2]) {
+    asm volatile(
+        "ds_read_b32 %0, %4\n\t"
+        "ds_read_b32 %1, %4 offset:64\n\t"
+        "ds_read_b32 %2, %5\n\t"
+        "ds_read_b32 %3, %5 offset:64\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(t[0]), "=&v"(t[1]), "=&v"(gt[0]), "=&v"(gt[1])
+        : "v"(lds_off(tau_base)), "v"(lds_off(gt_base))
+        : "memory");
+}
+
+// key-in-accumulator versions of epi_push / epi_retry
+template <int M, int N>
+__device__ __forceinline__ bool epi3_push(const f32x4 (&acc)[M][N], const int (&qloc)[N], const float (&tn)[N],
+                                          int rl0, int rlim, int trow0, unsigned (&pend)[N], float* lst_d,
+                                          int* lst_i, int* cnt) {
+    bool any = false;
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+        float mn = acc[0][n][0];
+#pragma unroll
+        for (int m = 0; m < M; ++m)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (m | i) mn = fminf(mn, acc[m][n][i]);
+        any |= mn <= tn[n];
+    }
+    if (!__any(any)) return false;
+    bool ovf = false;
+#pragma unroll
+    for (int n = 0; n < N; ++n)
+#pragma unroll
+        for (int m = 0; m < M; ++m)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float v = acc[m][n][i];
+                const int rl = rl0 + m * 16 + i;
+                if (rl < rlim && v <= tn[n]) {
+                    const int s = atomicAdd(&cnt[qloc[n]], 1);
+                    if (s < CAP) {
+                        lst_d[qloc[n] * CAP + s] = v;
+                        lst_i[qloc[n] * CAP + s] = trow0 + rl;
+                    } else {
+                        pend[n] |= 1u << (m * 4 + i);
+                        ovf = true;
+                    }
+                }
+            }
+    return ovf;
+}
+
+template <int M, int N>
+__device__ __forceinline__ bool epi3_retry(const f32x4 (&acc)[M][N], const int (&qloc)[N], const float (&tn)[N],
+                                           int rl0, int trow0, unsigned (&pend)[N], float* lst_d, int* lst_i,
+                                           int* cnt) {
+    bool ovf = false;
+#pragma unroll
+    for (int n = 0; n < N; ++n)
+#pragma unroll
+        for (int m = 0; m < M; ++m)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const unsigned bit = 1u << (m * 4 + i);
+                if (pend[n] & bit) {
+                    const float v = acc[m][n][i];
+                    pend[n] &= ~bit;
+                    if (v <= tn[n]) {
+                        const int s = atomicAdd(&cnt[qloc[n]], 1);
+                        if (s < CAP) {
+                            lst_d[qloc[n] * CAP + s] = v;
+                            lst_i[qloc[n] * CAP + s] = trow0 + rl0 + m * 16 + i;
+                        } else {
+                            pend[n] |= bit;
+                            ovf = true;
+                        }
+                    }
+                }
+            }
+    return ovf;
+}
+
+template <int DT, int METRIC, int KSTEPS>
+__global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_q3(ScanParams p) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    typedef typename AsmMmaV<DT>::A frag_t;
+    typedef typename AsmMmaV<DT>::B bfrag_t;
+    constexpr int SPT = KSTEPS / 2;
+    constexpr int NS = V2_NS;
+    constexpr int M = TILE_R / 16;
+    constexpr int N = 2;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int qtile, split;
+    map_block(blockIdx.x, p, qtile, split);
+    if (qtile >= p.n_qtiles) return;
+    const int ct0 = (int)((int64_t)split * p.n_ctiles / p.splits);
+    const int ct1 = (int)((int64_t)(split + 1) * p.n_ctiles / p.splits);
+    const int ntiles = ct1 - ct0;
+    const int64_t q0 = (int64_t)qtile * TILE_Q;
+    constexpr int rb = KSTEPS * 64;
+
+    float* lst_d = (float*)(smem + V2_LD_OFF);
+    int* lst_i = (int*)(smem + V2_LI_OFF);
+    int* cnt = (int*)(smem + V2_CNT_OFF);
+    float* tau = (float*)(smem + V2_TAU_OFF);
+    volatile int* flag = (volatile int*)(smem + V2_FLAG_OFF);
+    for (int x = tid; x < TILE_Q; x += SCAN_THREADS) { cnt[x] = 0; tau[x] = FX_INF; }
+    if (tid == 0) *flag = 0;
+
+    bfrag_t b[KSTEPS][N];
+    {
+        const char* qb = p.qop + (q0 + wave * 32 + (lane & 15)) * rb + (lane >> 4) * 16;
+#pragma unroll
+        for (int ks = 0; ks < KSTEPS; ++ks)
+#pragma unroll
+            for (int n = 0; n < N; ++n) b[ks][n] = *(const bfrag_t*)(qb + n * 16 * rb + ks * 64);
+    }
+    int offs[4];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+        const int bi = wave * 4 + jj, rblk = bi >> 1, kb = bi & 1;
+        offs[jj] = (rblk * 16 + (lane & 15)) * rb + kb * 64 + (lane >> 4) * 16;
+    }
+    const unsigned* gtq = p.gtau + q0 + wave * 32;
+    // DMA piece `which` (0-3 corpus blocks, 4 norms + shared thresholds) of stage g
+    auto issue_piece = [&](int g, int which) {
+        int t = g / SPT;
+        const int j = g - t * SPT;
+        if (t >= ntiles) t = ntiles - 1;  // dummy stage: uniform vmcnt accounting
+        const int64_t row0 = (int64_t)(ct0 + t) * TILE_R;
+        if (which < 4) {
+            glds16(p.codes + row0 * rb + j * STAGE_B + offs[which],
+                   smem + (g % NS) * V2_STAGE + (wave * 4 + which) * 1024);
+        } else if (lane < 16) {
+            const void* src = lane < 8 ? (const void*)(p.norms + row0 + wave * 32 + lane * 4)
+                                       : (const void*)(gtq + (lane - 8) * 4);
+            glds16(src, smem + V2_NORM_OFF + (t & 3) * V2_SLOT_B + wave * 256);
+        }
+    };
+    auto read_half = [&](int g, int kb, frag_t (&a)[M]) {
+        const char* slot = smem + (g % NS) * V2_STAGE;
+#pragma unroll
+        for (int m = 0; m < M; ++m) a[m] = *(const frag_t*)(slot + (m * 2 + kb) * 1024 + lane * 16);
+    };
+
+#pragma unroll
+    for (int st = 0; st < NS - 1; ++st)
+#pragma unroll
+        for (int w = 0; w < 5; ++w) issue_piece(st, w);
+
+    f32x4 acc[M][N];
+    const int rl0 = 4 * (lane >> 4);
+    int qloc[N];
+#pragma unroll
+    for (int n = 0; n < N; ++n) qloc[n] = wave * 32 + n * 16 + (lane & 15);
+    const bool qv0 = q0 + qloc[0] < p.nq, qv1 = q0 + qloc[1] < p.nq;
+    unsigned pend[N] = {0u, 0u};
+
+    auto overflow = [&](int tp) {
+        const int trow0 = (ct0 + tp) * TILE_R;
+        while (*flag) {
+            __syncthreads();
+            if (tid == 0) *flag = 0;
+            compact_full(lst_d, lst_i, cnt, tau, wave, lane, p.gtau + q0);
+            __syncthreads();
+            float tn[N];
+#pragma unroll
+            for (int n = 0; n < N; ++n) tn[n] = tau[qloc[n]];
+            if (epi3_retry<M, N>(acc, qloc, tn, rl0, trow0, pend, lst_d, lst_i, cnt)) *flag = 1;
+            __syncthreads();
+        }
+    };
+
+    frag_t s0[M], s1[M], s2[M];
+    const int G = ntiles * SPT;
+    asm volatile("s_waitcnt vmcnt(15)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (G > 0) {
+        read_half(0, 0, s0);
+        read_half(0, 1, s1);
+    }
+
+    for (int t = 0; t < ntiles; ++t) {
+#pragma unroll
+        for (int j = 0; j < SPT; ++j) {
+            const int g = t * SPT + j;
+            const int rx = (2 * j) % 3, ry = (2 * j + 1) % 3;  // sets of this stage's halves
+            frag_t (&X)[M] = rx == 0 ? s0 : (rx == 1 ? s1 : s2);
+            frag_t (&Y)[M] = ry == 0 ? s0 : (ry == 1 ? s1 : s2);
+            frag_t (&Z)[M] = (3 - rx - ry) == 0 ? s0 : ((3 - rx - ry) == 1 ? s1 : s2);
+            // stage g+1 landed for every wave; slot (g-1)%NS is free for the DMA
+            asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            f32x4 yinit[M];
+            if (j == 0) {
+                if (METRIC == L2) {
+                    lds_read_norms(smem + V2_NORM_OFF + (t & 3) * V2_SLOT_B + rl0 * 4, yinit);
+                } else {
+#pragma unroll
+                    for (int m = 0; m < M; ++m) yinit[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+                }
+            }
+            if (j + 1 < SPT) read_half(g + 1, 0, Z);
+            issue_piece(g + NS - 1, 0);
+            issue_piece(g + NS - 1, 1);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int m = 0; m < M; ++m)
+#pragma unroll
+                for (int n = 0; n < N; ++n) {
+                    if (j == 0) AsmMmaV<DT>::mmac(acc[m][n], X[m], b[0][n], yinit[m]);
+                    else AsmMmaV<DT>::mma(acc[m][n], X[m], b[2 * j][n]);
+                }
+            __builtin_amdgcn_sched_barrier(0);
+            issue_piece(g + NS - 1, 2);
+            issue_piece(g + NS - 1, 3);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int m = 0; m < M / 2; ++m)
+#pragma unroll
+                for (int n = 0; n < N; ++n) AsmMmaV<DT>::mma(acc[m][n], Y[m], b[2 * j + 1][n]);
+            __builtin_amdgcn_sched_barrier(0);
+            // X's last readers were issued >= 8 MFMAs ago: safe to overwrite
+            if (j + 1 < SPT) read_half(g + 1, 1, X);
+            issue_piece(g + NS - 1, 4);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int m = M / 2; m < M; ++m)
+#pragma unroll
+                for (int n = 0; n < N; ++n) AsmMmaV<DT>::mma(acc[m][n], Y[m], b[2 * j + 1][n]);
+        }
+        // epilogue: the accumulator holds the keys
+        acc_fence_v(acc);
+        {
+            float tn[N];
+            unsigned gt[N];
+            const char* nb = smem + V2_NORM_OFF + (t & 3) * V2_SLOT_B;
+            lds_read_tau(tau + qloc[0], nb + wave * 256 + 128 + (lane & 15) * 4, tn, gt);
+            tn[0] = qv0 ? fminf(tn[0], ord2f(gt[0])) : -FX_INF;
+            tn[1] = qv1 ? fminf(tn[1], ord2f(gt[1])) : -FX_INF;
+            const int trow0 = (ct0 + t) * TILE_R;
+            const int rlim = (int)(p.ntotal - (int64_t)trow0);
+            if (epi3_push<M, N>(acc, qloc, tn, rl0, rlim, trow0, pend, lst_d, lst_i, cnt)) *flag = 1;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        if (lds_read_flag(flag)) overflow(t);
+        if (t + 1 < ntiles) {
+            read_half((t + 1) * SPT, 0, s0);
+            read_half((t + 1) * SPT, 1, s1);
+        }
+    }
+
     // final flush: sorted top-KP per query of this (query tile, split)
     __syncthreads();
     const int64_t obase = ((int64_t)qtile * p.splits + split) * TILE_Q;
@@ -1146,11 +1491,19 @@ static hipError_t scan_t(const ScanParams& p, hipStream_t s) {
 
 template <int DT, int METRIC, int KSTEPS>
 static hipError_t scan_v2_t(const ScanParams& p, hipStream_t s) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_scan_qreg<DT, METRIC, KSTEPS>,
+    const int grid = p.qt_per_xcd > 0 ? 8 * p.qt_per_xcd * p.splits : p.n_qtiles * p.splits;
+    static const bool use_v2 = getenv("FX_SCAN_V2") != nullptr;
+    if (use_v2) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_scan_qreg<DT, METRIC, KSTEPS>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, V2_LDS_BYTES);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL((k_scan_qreg<DT, METRIC, KSTEPS>), dim3(grid), dim3(SCAN_THREADS), V2_LDS_BYTES, s, p);
+        return hipGetLastError();
+    }
+    hipError_t e = hipFuncSetAttribute((const void*)k_scan_q3<DT, METRIC, KSTEPS>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, V2_LDS_BYTES);
     if (e != hipSuccess) return e;
-    const int grid = p.qt_per_xcd > 0 ? 8 * p.qt_per_xcd * p.splits : p.n_qtiles * p.splits;
-    hipLaunchKernelGGL((k_scan_qreg<DT, METRIC, KSTEPS>), dim3(grid), dim3(SCAN_THREADS), V2_LDS_BYTES, s, p);
+    hipLaunchKernelGGL((k_scan_q3<DT, METRIC, KSTEPS>), dim3(grid), dim3(SCAN_THREADS), V2_LDS_BYTES, s, p);
     return hipGetLastError();
 }
 

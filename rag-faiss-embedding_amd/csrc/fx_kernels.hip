@@ -863,6 +863,7 @@ template <int DT> struct AsmMmaV;
 template <> struct AsmMmaV<BF16> {
     typedef bf16x8 A;
     typedef bf16x8 B;
+    static __device__ __forceinline__ void settle(const B& b) { asm volatile("" ::"a"(b)); }
     static __device__ __forceinline__ void mma(f32x4& c, const A& a, const B& b) {
         asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "a"(b));
     }
@@ -873,6 +874,7 @@ template <> struct AsmMmaV<BF16> {
 template <> struct AsmMmaV<F16> {
     typedef f16x8 A;
     typedef f16x8 B;
+    static __device__ __forceinline__ void settle(const B& b) { asm volatile("" ::"a"(b)); }
     static __device__ __forceinline__ void mma(f32x4& c, const A& a, const B& b) {
         asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "a"(b));
     }
@@ -883,6 +885,9 @@ template <> struct AsmMmaV<F16> {
 template <> struct AsmMmaV<F32> {
     typedef f32x4 A;
     typedef Bf32 B;
+    static __device__ __forceinline__ void settle(const B& b) {
+        asm volatile("" ::"a"(b.x[0]), "a"(b.x[1]), "a"(b.x[2]), "a"(b.x[3]));
+    }
     static __device__ __forceinline__ void mma(f32x4& c, const A& a, const B& b) {
         asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(c) : "v"(a[0]), "a"(b.x[0]));
         asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(c) : "v"(a[1]), "a"(b.x[1]));
@@ -921,6 +926,49 @@ __device__ __forceinline__ void lds_read_norms(const char* base, f32x4 (&y)[8]) 
         : "=&v"(y[0]), "=&v"(y[1]), "=&v"(y[2]), "=&v"(y[3]), "=&v"(y[4]), "=&v"(y[5]), "=&v"(y[6]), "=&v"(y[7])
         : "v"(lds_off(base))
         : "memory");
+}
+// LDS-DMA of one 1 KiB block (16 B per lane) issued from inline asm: the
+// compiler then tracks no VMEM->LDS event and inserts none of its own
+// conservative vmcnt(0) drains; the scan loops' counted barrier waits are the
+// only synchronisation (MI355X_MICROARCH.md, LDS-DMA section).
+__device__ __forceinline__ void glds16_asm(const void* gsrc, uint32_t lds_uniform) {
+    asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+                 :
+                 : "v"(gsrc), "{m0}"(__builtin_amdgcn_readfirstlane(lds_uniform))
+                 : "memory");
+}
+// Eight ds_read_b128 of one ring half-stage with NO wait: the consumer MFMAs run
+// only after the next counted barrier (s_waitcnt ... lgkmcnt(0); s_barrier).
+template <int KB, typename T>
+__device__ __forceinline__ void lds_read_half_nowait(uint32_t base, T (&a)[8]) {
+#define FX_HR(o) "ds_read_b128 %0, %8 offset:" #o "\n\t"
+    if (KB == 0)
+        asm volatile("ds_read_b128 %0, %8\n\t"
+                     "ds_read_b128 %1, %8 offset:2048\n\t"
+                     "ds_read_b128 %2, %8 offset:4096\n\t"
+                     "ds_read_b128 %3, %8 offset:6144\n\t"
+                     "ds_read_b128 %4, %8 offset:8192\n\t"
+                     "ds_read_b128 %5, %8 offset:10240\n\t"
+                     "ds_read_b128 %6, %8 offset:12288\n\t"
+                     "ds_read_b128 %7, %8 offset:14336"
+                     : "=&v"(a[0]), "=&v"(a[1]), "=&v"(a[2]), "=&v"(a[3]), "=&v"(a[4]), "=&v"(a[5]), "=&v"(a[6]),
+                       "=&v"(a[7])
+                     : "v"(base)
+                     : "memory");
+    else
+        asm volatile("ds_read_b128 %0, %8 offset:1024\n\t"
+                     "ds_read_b128 %1, %8 offset:3072\n\t"
+                     "ds_read_b128 %2, %8 offset:5120\n\t"
+                     "ds_read_b128 %3, %8 offset:7168\n\t"
+                     "ds_read_b128 %4, %8 offset:9216\n\t"
+                     "ds_read_b128 %5, %8 offset:11264\n\t"
+                     "ds_read_b128 %6, %8 offset:13312\n\t"
+                     "ds_read_b128 %7, %8 offset:15360"
+                     : "=&v"(a[0]), "=&v"(a[1]), "=&v"(a[2]), "=&v"(a[3]), "=&v"(a[4]), "=&v"(a[5]), "=&v"(a[6]),
+                       "=&v"(a[7])
+                     : "v"(base)
+                     : "memory");
+#undef FX_HR
 }
 __device__ __forceinline__ void lds_read_tau(const float* tau_base, const char* gt_base, float (&t)[2],
                                              unsigned (&gt)[2]) {
@@ -1040,6 +1088,12 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_q3(ScanParams p) {
         for (int ks = 0; ks < KSTEPS; ++ks)
 #pragma unroll
             for (int n = 0; n < N; ++n) b[ks][n] = *(const bfrag_t*)(qb + n * 16 * rb + ks * 64);
+        // settle the operand loads here, once: otherwise the compiler re-waits
+        // (vmcnt(0), draining the corpus DMA ring) at every tile's first MFMA
+#pragma unroll
+        for (int ks = 0; ks < KSTEPS; ++ks)
+#pragma unroll
+            for (int n = 0; n < N; ++n) AsmMmaV<DT>::settle(b[ks][n]);
     }
     int offs[4];
 #pragma unroll
@@ -1048,6 +1102,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_q3(ScanParams p) {
         offs[jj] = (rblk * 16 + (lane & 15)) * rb + kb * 64 + (lane >> 4) * 16;
     }
     const unsigned* gtq = p.gtau + q0 + wave * 32;
+    const uint32_t lds_base = lds_off(smem);
     // DMA piece `which` (0-3 corpus blocks, 4 norms + shared thresholds) of stage g
     auto issue_piece = [&](int g, int which) {
         int t = g / SPT;
@@ -1055,18 +1110,18 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_q3(ScanParams p) {
         if (t >= ntiles) t = ntiles - 1;  // dummy stage: uniform vmcnt accounting
         const int64_t row0 = (int64_t)(ct0 + t) * TILE_R;
         if (which < 4) {
-            glds16(p.codes + row0 * rb + j * STAGE_B + offs[which],
-                   smem + (g % NS) * V2_STAGE + (wave * 4 + which) * 1024);
+            glds16_asm(p.codes + row0 * rb + j * STAGE_B + offs[which],
+                       lds_base + (g % NS) * V2_STAGE + (wave * 4 + which) * 1024);
         } else if (lane < 16) {
             const void* src = lane < 8 ? (const void*)(p.norms + row0 + wave * 32 + lane * 4)
                                        : (const void*)(gtq + (lane - 8) * 4);
-            glds16(src, smem + V2_NORM_OFF + (t & 3) * V2_SLOT_B + wave * 256);
+            glds16_asm(src, lds_base + V2_NORM_OFF + (t & 3) * V2_SLOT_B + wave * 256);
         }
     };
     auto read_half = [&](int g, int kb, frag_t (&a)[M]) {
-        const char* slot = smem + (g % NS) * V2_STAGE;
-#pragma unroll
-        for (int m = 0; m < M; ++m) a[m] = *(const frag_t*)(slot + (m * 2 + kb) * 1024 + lane * 16);
+        const uint32_t slot = lds_base + (g % NS) * V2_STAGE + lane * 16;
+        if (kb == 0) lds_read_half_nowait<0>(slot, a);
+        else lds_read_half_nowait<1>(slot, a);
     };
 
 #pragma unroll

@@ -238,7 +238,7 @@ def main():
         roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(gbs / HBM_PEAK_GBS, 4)}
     roof["traffic"] = read_pmc_traffic(args.config, n_local, nq)
-    roof["kernel"] = "k_scan_qreg (fused MFMA distance GEMM + top-k select)"
+    roof["kernel"] = "k_scan_v4 (fused MFMA distance GEMM + top-k select)"
     roof["kernel_ms_avg"] = round(scan_avg_ms, 4)
     roof["launches"] = launches
     roof["merge_refine_ms_avg"] = round(merge_ms / max(launches, 1), 4)

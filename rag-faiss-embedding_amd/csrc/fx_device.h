@@ -1,0 +1,282 @@
+// fx_device.h -- device-side helpers shared by the HIP translation units
+// (fx_kernels.hip: add/refine/merge/synth + generic scan; fx_scan.hip: the
+// MFMA scan).  Header-only, all inline.
+#pragma once
+#include "fx_internal.h"
+
+#include <float.h>
+#include <limits.h>
+
+namespace fx {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define FX_INF __builtin_inff()
+
+// ---------------------------------------------------------------------------
+// scalar conversions
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+__device__ __forceinline__ uint16_t f2bf(float f) {  // round to nearest even, NaN kept NaN
+    uint32_t u = __float_as_uint(f);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40u);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+__device__ __forceinline__ float h2f(uint16_t h) {
+    _Float16 x;
+    __builtin_memcpy(&x, &h, 2);
+    return (float)x;
+}
+__device__ __forceinline__ uint16_t f2h(float f) {
+    _Float16 x = (_Float16)f;
+    uint16_t h;
+    __builtin_memcpy(&h, &x, 2);
+    return h;
+}
+
+__device__ __forceinline__ float load_elem(const void* p, int64_t idx, int dt) {
+    if (dt == F32) return ((const float*)p)[idx];
+    uint16_t h = ((const uint16_t*)p)[idx];
+    return dt == BF16 ? bf2f(h) : h2f(h);
+}
+// round v to dtype dt and back (the value the index stores)
+__device__ __forceinline__ float round_to(float v, int dt) {
+    if (dt == F32) return v;
+    return dt == BF16 ? bf2f(f2bf(v)) : h2f(f2h(v));
+}
+__device__ __forceinline__ void store_elem(void* p, int64_t idx, int dt, float v) {
+    if (dt == F32) ((float*)p)[idx] = v;
+    else ((uint16_t*)p)[idx] = dt == BF16 ? f2bf(v) : f2h(v);
+}
+
+// ---------------------------------------------------------------------------
+// wave-level (64-lane) bitonic helpers on (key, id) pairs, ascending,
+// ties -> smaller id.  Used for LDS list compaction and every merge.
+// ---------------------------------------------------------------------------
+template <typename Id>
+__device__ __forceinline__ bool key_lt(float d1, Id i1, float d2, Id i2) {
+    return d1 < d2 || (d1 == d2 && i1 < i2);
+}
+
+template <typename Id>
+__device__ __forceinline__ void cmpx(float& d, Id& i, int lane, int stride, bool asc) {
+    float od = __shfl_xor(d, stride, 64);
+    Id oi = __shfl_xor(i, stride, 64);
+    bool lower = (lane & stride) == 0;
+    bool take = (lower == asc) ? key_lt(od, oi, d, i) : key_lt(d, i, od, oi);
+    d = take ? od : d;
+    i = take ? oi : i;
+}
+
+template <typename Id>
+__device__ __forceinline__ void sort64(float& d, Id& i, int lane) {
+#pragma unroll
+    for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+        for (int stride = size >> 1; stride > 0; stride >>= 1) cmpx(d, i, lane, stride, (lane & size) == 0);
+    }
+}
+
+template <typename Id>
+__device__ __forceinline__ void merge64(float& d, Id& i, int lane) {  // bitonic -> ascending
+#pragma unroll
+    for (int stride = 32; stride > 0; stride >>= 1) cmpx(d, i, lane, stride, true);
+}
+
+// best (ascending, one per lane) <- the 64 smallest of best U cand (cand sorted ascending)
+template <typename Id>
+__device__ __forceinline__ void merge_into(float& bd, Id& bi, float cd, Id ci, int lane) {
+    float rd = __shfl(cd, 63 - lane, 64);
+    Id ri = __shfl(ci, 63 - lane, 64);
+    if (key_lt(rd, ri, bd, bi)) { bd = rd; bi = ri; }
+    merge64(bd, bi, lane);
+}
+
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ float wave_sum_f32(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+
+// LDS byte offset of a generic pointer into the extern LDS array
+__device__ __forceinline__ uint32_t lds_off(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+__device__ __forceinline__ void glds16(const void* gsrc, char* lds_uniform) {
+    __builtin_amdgcn_global_load_lds(gsrc, (__attribute__((address_space(3))) void*)lds_uniform, 16, 0, 0);
+}
+
+// blockIdx -> (query tile, corpus split).  With >= 8 query tiles the grid is
+// laid out so that, under the observed round-robin dispatch of blocks over the
+// 8 XCDs, each XCD group owns a fixed set of query tiles (their operand stays
+// in that XCD's L2) and all groups walk the corpus splits in the same order
+// (corpus rows are fetched from HBM about once and re-read from L2/MALL).
+// Placement only changes speed, never results.
+__device__ __forceinline__ void map_block(int b, const ScanParams& p, int& qtile, int& split) {
+    if (p.qt_per_xcd > 0) {
+        int xcd = b & 7, j = b >> 3;
+        qtile = xcd + 8 * (j % p.qt_per_xcd);
+        split = j / p.qt_per_xcd;
+    } else {
+        qtile = b % p.n_qtiles;
+        split = b / p.n_qtiles;
+    }
+}
+
+// diagnostics (FX_SCAN_TRACE): where and when each block ran
+__device__ __noinline__ void trace_block_start(const ScanParams& p, int qtile, int split) {
+    unsigned xcc, hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    unsigned long long* t = p.trace + blockIdx.x * 4;
+    t[0] = (unsigned long long)(xcc & 0xf) | ((unsigned long long)(hw & 0xffffff) << 8) |
+           ((unsigned long long)qtile << 32);
+    t[1] = (unsigned long long)split;
+    t[2] = wall_clock64();
+}
+
+// order-preserving float <-> uint (atomicMin on floats of either sign)
+__device__ __forceinline__ unsigned f2ord(float f) {
+    const unsigned u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float ord2f(unsigned o) {
+    return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
+}
+
+// Compact every full list (cnt >= CAP) to its KP best entries; tau = KP-th.
+__device__ __forceinline__ void compact_full(float* lst_d, int* lst_i, int* cnt, float* tau, int wave, int lane,
+                                             unsigned* gtau = nullptr) {
+    for (int q = wave; q < TILE_Q; q += 4) {
+        if (cnt[q] >= CAP) {
+            float d = lst_d[q * CAP + lane];
+            int i = lst_i[q * CAP + lane];
+            sort64(d, i, lane);
+            if (lane < KP) { lst_d[q * CAP + lane] = d; lst_i[q * CAP + lane] = i; }
+            if (lane == KP - 1) {
+                tau[q] = d;
+                // publish: no split needs keys above the best KP-th of any split
+                if (gtau) atomicMin(gtau + q, f2ord(d));
+            }
+            if (lane == 0) cnt[q] = KP;
+        }
+    }
+}
+
+// f32: a 64-B k-chunk is 4 k-steps of 16x16x4 (see Frag<F32>); B is kept as 4
+// scalar AGPRs per chunk.
+struct Bf32 { float x[4]; };
+
+// MFMAs as inline asm (the B operand pinned in AGPRs: the builtin form left
+// the stationary query fragments to the allocator, which spilled them).
+// Accumulators are "+v" operands even where srcC is an initialiser, so they
+// keep fixed registers across tiles.  mma2* issue the two query columns n = 0,
+// 1 of one A fragment; INIT: 0 accumulate, 1 srcC = c_init (row norms), 2
+// srcC = 0.  hipcc does not see the latency of these MFMAs: every register
+// they read must stay unwritten until they have read it (the scan keeps its
+// operand registers live and pinned, see fx_scan.hip) and acc_fence_v pads
+// the XDL-write -> VALU-read wait states before an epilogue reads them.
+template <int DT> struct AsmMmaV;
+template <> struct AsmMmaV<BF16> {
+    typedef bf16x8 A;
+    typedef bf16x8 B;
+    static __device__ __forceinline__ void settle(const B& b) { asm volatile("" ::"a"(b)); }
+    template <int INIT>
+    static __device__ __forceinline__ void mma2(f32x4& c0, f32x4& c1, const A& a, const B& b0, const B& b1,
+                                                const f32x4& ci) {
+        if constexpr (INIT == 0) {
+            asm volatile("v_mfma_f32_16x16x32_bf16 %0, %2, %3, %0\n\t"
+                         "v_mfma_f32_16x16x32_bf16 %1, %2, %4, %1"
+                         : "+v"(c0), "+v"(c1) : "v"(a), "a"(b0), "a"(b1));
+        } else if constexpr (INIT == 1) {
+            asm volatile("v_mfma_f32_16x16x32_bf16 %0, %2, %3, %5\n\t"
+                         "v_mfma_f32_16x16x32_bf16 %1, %2, %4, %5"
+                         : "+v"(c0), "+v"(c1) : "v"(a), "a"(b0), "a"(b1), "v"(ci));
+        } else {
+            asm volatile("v_mfma_f32_16x16x32_bf16 %0, %2, %3, 0\n\t"
+                         "v_mfma_f32_16x16x32_bf16 %1, %2, %4, 0"
+                         : "+v"(c0), "+v"(c1) : "v"(a), "a"(b0), "a"(b1));
+        }
+    }
+};
+template <> struct AsmMmaV<F16> {
+    typedef f16x8 A;
+    typedef f16x8 B;
+    static __device__ __forceinline__ void settle(const B& b) { asm volatile("" ::"a"(b)); }
+    template <int INIT>
+    static __device__ __forceinline__ void mma2(f32x4& c0, f32x4& c1, const A& a, const B& b0, const B& b1,
+                                                const f32x4& ci) {
+        if constexpr (INIT == 0) {
+            asm volatile("v_mfma_f32_16x16x32_f16 %0, %2, %3, %0\n\t"
+                         "v_mfma_f32_16x16x32_f16 %1, %2, %4, %1"
+                         : "+v"(c0), "+v"(c1) : "v"(a), "a"(b0), "a"(b1));
+        } else if constexpr (INIT == 1) {
+            asm volatile("v_mfma_f32_16x16x32_f16 %0, %2, %3, %5\n\t"
+                         "v_mfma_f32_16x16x32_f16 %1, %2, %4, %5"
+                         : "+v"(c0), "+v"(c1) : "v"(a), "a"(b0), "a"(b1), "v"(ci));
+        } else {
+            asm volatile("v_mfma_f32_16x16x32_f16 %0, %2, %3, 0\n\t"
+                         "v_mfma_f32_16x16x32_f16 %1, %2, %4, 0"
+                         : "+v"(c0), "+v"(c1) : "v"(a), "a"(b0), "a"(b1));
+        }
+    }
+};
+// f32: a 64-B k-chunk is 4 k-steps of 16x16x4; the two columns' dependent
+// chains are interleaved (40-cycle dependent latency vs 32-cycle issue)
+template <> struct AsmMmaV<F32> {
+    typedef f32x4 A;
+    typedef Bf32 B;
+    static __device__ __forceinline__ void settle(const B& b) {
+        asm volatile("" ::"a"(b.x[0]), "a"(b.x[1]), "a"(b.x[2]), "a"(b.x[3]));
+    }
+    template <int INIT>
+    static __device__ __forceinline__ void mma2(f32x4& c0, f32x4& c1, const A& a, const B& b0, const B& b1,
+                                                const f32x4& ci) {
+#define FX_F32_TAIL                                            \
+    "v_mfma_f32_16x16x4_f32 %0, %3, %7, %0\n\t"                \
+    "v_mfma_f32_16x16x4_f32 %1, %3, %11, %1\n\t"               \
+    "v_mfma_f32_16x16x4_f32 %0, %4, %8, %0\n\t"                \
+    "v_mfma_f32_16x16x4_f32 %1, %4, %12, %1\n\t"               \
+    "v_mfma_f32_16x16x4_f32 %0, %5, %9, %0\n\t"                \
+    "v_mfma_f32_16x16x4_f32 %1, %5, %13, %1"
+#define FX_F32_OPS                                                                                      \
+    : "+v"(c0), "+v"(c1)                                                                                \
+    : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "a"(b0.x[0]), "a"(b0.x[1]), "a"(b0.x[2]), "a"(b0.x[3]), \
+      "a"(b1.x[0]), "a"(b1.x[1]), "a"(b1.x[2]), "a"(b1.x[3]), "v"(ci)
+        // operands: %2..%5 = a[0..3], %6..%9 = b0, %10..%13 = b1, %14 = ci
+        if constexpr (INIT == 0) {
+            asm volatile("v_mfma_f32_16x16x4_f32 %0, %2, %6, %0\n\t"
+                         "v_mfma_f32_16x16x4_f32 %1, %2, %10, %1\n\t" FX_F32_TAIL FX_F32_OPS);
+        } else if constexpr (INIT == 1) {
+            asm volatile("v_mfma_f32_16x16x4_f32 %0, %2, %6, %14\n\t"
+                         "v_mfma_f32_16x16x4_f32 %1, %2, %10, %14\n\t" FX_F32_TAIL FX_F32_OPS);
+        } else {
+            asm volatile("v_mfma_f32_16x16x4_f32 %0, %2, %6, 0\n\t"
+                         "v_mfma_f32_16x16x4_f32 %1, %2, %10, 0\n\t" FX_F32_TAIL FX_F32_OPS);
+        }
+#undef FX_F32_TAIL
+#undef FX_F32_OPS
+    }
+};
+
+// 48 wait states: covers the XDL-write -> VALU-read distance of the slowest
+// scan MFMA (16x16x4 f32 chain, 40-cycle dependent latency)
+__device__ __forceinline__ void acc_fence_v(f32x4 (&acc)[8][2]) {
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7"
+                 : "+v"(acc[0][0]), "+v"(acc[0][1]), "+v"(acc[1][0]), "+v"(acc[1][1]), "+v"(acc[2][0]),
+                   "+v"(acc[2][1]), "+v"(acc[3][0]), "+v"(acc[3][1]), "+v"(acc[4][0]), "+v"(acc[4][1]),
+                   "+v"(acc[5][0]), "+v"(acc[5][1]), "+v"(acc[6][0]), "+v"(acc[6][1]), "+v"(acc[7][0]),
+                   "+v"(acc[7][1]));
+}
+
+}  // namespace fx

@@ -92,7 +92,7 @@ struct FxIndex {
     hipStream_t own_stream = nullptr;
     hipStream_t user_stream = nullptr;
     // search workspace
-    DevBuf qin, qf32, qop, qeps, cand_d, cand_i, dws, iws, flag, fbc_d, fbc_i, stage, gtau;
+    DevBuf qin, qf32, qop, qeps, cand_d, cand_i, dws, iws, flag, fbc_d, fbc_i, stage, gtau, trace, dbgbuf;
     int64_t last_fallbacks = 0;
     // profiling
     bool profile = false;
@@ -202,6 +202,22 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
     HIP_TRY(h->cand_i.ensure(ncand * 4));
     sp.cand_d = (float*)h->cand_d.p;
     sp.cand_i = (int*)h->cand_i.p;
+    // diagnostics: per-block placement/timing of the scan -> binary file
+    const char* trace_path = getenv("FX_SCAN_TRACE");
+    const size_t grid = (size_t)(sp.qt_per_xcd > 0 ? 8 * sp.qt_per_xcd : sp.n_qtiles) * sp.splits;
+    sp.trace = nullptr;
+    sp.dbgbuf = nullptr;
+    const size_t nkeys = (size_t)sp.n_qtiles * TILE_Q * sp.n_ctiles * TILE_R;
+    if ((sp.dbg & 32) && nkeys <= (size_t)1 << 26) {
+        HIP_TRY(h->dbgbuf.ensure(nkeys * 4));
+        HIP_TRY(hipMemsetAsync(h->dbgbuf.p, 0xff, nkeys * 4, s));
+        sp.dbgbuf = (unsigned*)h->dbgbuf.p;
+    }
+    if (trace_path) {
+        HIP_TRY(h->trace.ensure(grid * 32));
+        HIP_TRY(hipMemsetAsync(h->trace.p, 0, grid * 32, s));
+        sp.trace = (unsigned long long*)h->trace.p;
+    }
 
     hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
     if (h->profile) {
@@ -255,6 +271,33 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
     HIP_TRY(hipMemcpyAsync(&nf, n_flag, 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     h->last_fallbacks = nf;
+    if (const char* cpath = getenv("FX_SCAN_CAND")) {  // diagnostics: raw scan candidate lists
+        std::vector<float> cd(ncand);
+        std::vector<int> ci(ncand);
+        HIP_TRY(hipMemcpy(cd.data(), sp.cand_d, ncand * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(ci.data(), sp.cand_i, ncand * 4, hipMemcpyDeviceToHost));
+        if (FILE* f = fopen(cpath, "wb")) {
+            fwrite(cd.data(), 4, ncand, f);
+            fwrite(ci.data(), 4, ncand, f);
+            fclose(f);
+        }
+    }
+    if (sp.dbgbuf) {  // diagnostics: the scan's key matrix [n_qtiles*128][n_ctiles*128] -> file
+        std::vector<float> kv(nkeys);
+        HIP_TRY(hipMemcpy(kv.data(), sp.dbgbuf, nkeys * 4, hipMemcpyDeviceToHost));
+        if (FILE* f = fopen(getenv("FX_SCAN_KEYS") ? getenv("FX_SCAN_KEYS") : "/tmp/fx_keys.bin", "wb")) {
+            fwrite(kv.data(), 4, kv.size(), f);
+            fclose(f);
+        }
+    }
+    if (sp.trace) {
+        std::vector<unsigned long long> tr(grid * 4);
+        HIP_TRY(hipMemcpy(tr.data(), sp.trace, grid * 32, hipMemcpyDeviceToHost));
+        if (FILE* f = fopen(trace_path, "wb")) {
+            fwrite(tr.data(), 8, tr.size(), f);
+            fclose(f);
+        }
+    }
     if (nf > 0 && sp.dbg == 0) {
         const int fb_splits = (int)std::max<int64_t>(1, std::min<int64_t>(256, (h->ntotal + 4095) / 4096));
         const int chunk = 64;
@@ -337,7 +380,7 @@ void fx_index_free(FxIndex* h) {
         if (h->norms) (void)hipFree(h->norms);
         if (h->max_sq_bits) (void)hipFree(h->max_sq_bits);
         for (DevBuf* b : {&h->qin, &h->qf32, &h->qop, &h->qeps, &h->cand_d, &h->cand_i, &h->dws, &h->iws, &h->flag,
-                          &h->fbc_d, &h->fbc_i, &h->stage, &h->gtau})
+                          &h->fbc_d, &h->fbc_i, &h->stage, &h->gtau, &h->trace, &h->dbgbuf})
             b->release();
         for (auto& pr : h->ev_scan) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
         for (auto& pr : h->ev_merge) (void)hipEventDestroy(pr.second);

@@ -47,6 +47,9 @@ struct ScanParams {
     int dbg;               // ablation switches (FX_SCAN_DBG; 0 in production)
     unsigned* gtau;        // [n_qtiles * TILE_Q] order-preserving bits of the best
                            // known KP-th key per query across splits (atomicMin)
+    unsigned long long* trace;  // diagnostics only (FX_SCAN_TRACE): per block
+                                // {xcc | hw_id << 8 | qtile << 32, split, t_start, t_end}
+    unsigned* dbgbuf;           // diagnostics only (FX_SCAN_DBG & 32): operand self-check
 };
 
 struct RefineParams {
@@ -75,6 +78,8 @@ hipError_t launch_prep_queries(const void* q, int q_dt, int64_t nq, int64_t nq_p
                                int st_dt, int metric, float* qf32, void* qop, float* qeps,
                                double max_norm, hipStream_t s);
 hipError_t launch_scan(int st_dt, int metric, const ScanParams& p, hipStream_t s);
+// fx_scan.hip: the MFMA scan; *handled = false when it has no kernel for p.row_bytes
+hipError_t launch_scan_mfma(int st_dt, int metric, const ScanParams& p, hipStream_t s, bool* handled);
 hipError_t launch_refine(int st_dt, int metric, const RefineParams& p, hipStream_t s);
 hipError_t launch_exact_fallback(int st_dt, int metric, const char* codes, int row_bytes, int kdim,
                                  int64_t ntotal, const float* qf32, const int* qlist, int nlist,

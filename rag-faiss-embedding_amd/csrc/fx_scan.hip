@@ -1,0 +1,460 @@
+// fx_scan.hip -- the search() hot loop on gfx950: exact squared-L2 / inner
+// product scan of the HBM-resident code matrix fused with a top-KP select.
+//
+// Replaces the arithmetic of faiss IndexFlatL2::search (faiss_store.py:64,
+// rag_datastore_manager.py:218 -> knn_L2sqr) for every row width that has a
+// register layout here (row_bytes / 64 in {8, 12, 16, 24}); other widths use
+// the generic kernel k_scan_topk in fx_kernels.hip.
+//
+// Workgroup = 4 waves, one per SIMD, one workgroup per CU (LDS-bound); work
+// item = (query tile of 128, corpus split).  Each wave keeps its 32 queries
+// stationary in AGPRs for the whole K (MFMA B operand, pre-scaled by -2 for L2
+// / -1 for IP so that the accumulator is the key) and streams the split's
+// corpus tiles (128 rows) through a 5-slot LDS ring in 128-B-of-K stages:
+//
+//   * corpus: LDS-DMA (global_load_lds_dwordx4), 4 x 1 KiB pieces per wave per
+//     stage with a scalar base (SGPR pair) + fixed per-lane offsets, so a
+//     piece costs one SALU add for M0 and no vector address arithmetic;
+//     the fragment-ordered LDS image makes every ds_read_b128 contiguous;
+//   * one counted `s_waitcnt vmcnt(10)` + s_barrier per stage (exactly 5 VMEM
+//     ops per wave per stage: 4 corpus pieces + 1 row-norm / shared-threshold
+//     piece), no other VMEM in the loop;
+//   * A fragments double-buffered in two register sets: half 1 of stage g is
+//     read during half 0's MFMAs, half 0 of stage g+1 during half 1's MFMAs;
+//   * a tile's first MFMA takes srcC = |y|^2 of its rows (L2), so after the
+//     tile the accumulator holds key = |y|^2 - 2 x.y directly;
+//   * epilogue: per-(query, 16-row group) minima, one ballot; the rare tiles
+//     with a candidate below the query's threshold push only the groups that
+//     hold one into that query's LDS list (lists are per wave: no workgroup
+//     barrier); a full list is compacted by a wave-level bitonic sort and its
+//     KP-th key is published to a per-query global threshold (atomicMin)
+//     shared by all corpus splits.
+#include "fx_device.h"
+
+#include <stdlib.h>
+
+#include <utility>
+
+namespace fx {
+
+constexpr int S_NS = 5;                         // ring slots (S_NS - 1 stages in flight)
+constexpr int S_STAGE = TILE_R * STAGE_B;       // 16 KiB = 128 rows x 128 B
+// norm / threshold slots first: every ring piece's LDS address is then >= 4 KiB,
+// more than any instruction offset subtracted from its M0 (see dma_piece)
+constexpr int S_NORM_OFF = 0;                   // 4 tile slots x 4 waves x 256 B
+constexpr int S_NSLOT_B = 4 * 256;              // [wave][32 row norms | 32 thresholds]
+constexpr int S_RING_OFF = S_NORM_OFF + 4 * S_NSLOT_B;
+constexpr int S_LD_OFF = S_RING_OFF + S_NS * S_STAGE;
+constexpr int S_LI_OFF = S_LD_OFF + TILE_Q * CAP * 4;
+constexpr int S_CNT_OFF = S_LI_OFF + TILE_Q * CAP * 4;
+constexpr int S_TAU_OFF = S_CNT_OFF + TILE_Q * 4;
+constexpr int S_LDS_BYTES = S_TAU_OFF + TILE_Q * 4;
+static_assert(S_LDS_BYTES <= 160 * 1024, "LDS budget");
+
+// Largest finite float: thresholds start here, so real keys always pass and
+// padding rows (|y|^2 = +inf -> key +inf) never do.
+constexpr float KEY_MAX = FLT_MAX;
+
+template <int... Is, typename F>
+__device__ __forceinline__ void static_for_impl(std::integer_sequence<int, Is...>, F&& f) {
+    (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    static_for_impl(std::make_integer_sequence<int, N>{}, f);
+}
+
+// one 1 KiB LDS-DMA piece: lane l moves 16 B from sbase + voff + OFF to
+// LDS[lds + 16 l].  The instruction offset is added to the LDS address as
+// well (LDS = M0 + OFF + 16 lane), so M0 is set to lds - OFF (>= 0: the ring
+// starts at 4 KiB, OFF < 1.5 KiB).  The s_nop is the M0-write -> LDS-DMA wait
+// state.
+template <int OFF>
+__device__ __forceinline__ void dma_piece(uint32_t voff, const char* sbase, uint32_t lds) {
+    static_assert(OFF >= 0 && OFF < S_RING_OFF, "M0 = lds - OFF must not wrap");
+    asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, %1 offset:%2" ::"v"(voff), "s"(sbase), "i"(OFF),
+                 "{m0}"(lds - OFF)
+                 : "memory");
+}
+// the per-stage row-norm / threshold piece: lanes 0-7 move 32 row norms,
+// lanes 8-15 the wave's 32 shared thresholds; lanes 16-63 are masked off
+__device__ __forceinline__ void dma_norm_piece(const char* vaddr, uint32_t m0) {
+    uint64_t saved;
+    asm volatile(
+        "s_mov_b64 %0, exec\n\t"
+        "s_mov_b64 exec, 0xffff\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\t"
+        "s_mov_b64 exec, %0"
+        : "=&s"(saved)
+        : "v"(vaddr), "{m0}"(m0)
+        : "memory");
+}
+// LDS -> MFMA operand registers.  "+v": the destination keeps its register
+// for the whole kernel (no other value is ever placed there), so the only
+// writes to an operand register are these reads, scheduled >= 8 MFMAs after
+// the register's last MFMA reader
+template <int OFF, typename T>
+__device__ __forceinline__ void ds_rd128(T& d, uint32_t addr) {
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "+v"(d) : "v"(addr), "i"(OFF) : "memory");
+}
+template <int OFF, typename T>
+__device__ __forceinline__ void ds_rd32(T& d, uint32_t addr) {
+    asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(d) : "v"(addr), "i"(OFF) : "memory");
+}
+
+// Compact this wave's full lists (cnt >= CAP) to their KP best; tau = KP-th,
+// published to the shared per-query threshold.  Lists are owned by one wave.
+__device__ __noinline__ void compact_wave(float* lst_d, int* lst_i, int* cnt, float* tau, unsigned* gtq, int qw0,
+                                          int lane) {
+    for (int qi = 0; qi < 32; ++qi) {
+        const int q = qw0 + qi;
+        if (cnt[q] >= CAP) {
+            float d = lst_d[q * CAP + lane];
+            int i = lst_i[q * CAP + lane];
+            sort64(d, i, lane);
+            if (lane < KP) {
+                lst_d[q * CAP + lane] = d;
+                lst_i[q * CAP + lane] = i;
+            }
+            if (lane == KP - 1) {
+                tau[q] = d;
+                atomicMin(gtq + qi, f2ord(d));
+            }
+            if (lane == 0) cnt[q] = KP;
+        }
+    }
+}
+
+// push the entries of accumulator group (m, n) selected by `elig` (4 bits)
+// that pass `tn` into query q's list; entries that find the list full are
+// recorded in `pend` (bit 4m+i) for a retry after compaction
+template <int M, int N>
+__device__ __forceinline__ bool push_group(const f32x4 (&acc)[M][N], int n, int m, unsigned elig, float tn, int q,
+                                           int row0, int rlim, float* lst_d, int* lst_i, int* cnt, unsigned& pend) {
+    bool ovf = false;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float v = acc[m][n][i];
+        const int rl = row0 + i;
+        if (((elig >> i) & 1u) && v <= tn && rl < rlim) {
+            const int s = atomicAdd(&cnt[q], 1);
+            if (s < CAP) {
+                lst_d[q * CAP + s] = v;
+                lst_i[q * CAP + s] = rl;
+            } else {
+                pend |= 1u << (m * 4 + i);
+                ovf = true;
+            }
+        }
+    }
+    return ovf;
+}
+
+template <int DT, int METRIC, int KSTEPS>
+__global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    typedef typename AsmMmaV<DT>::A frag_t;
+    typedef typename AsmMmaV<DT>::B bfrag_t;
+    constexpr int SPT = KSTEPS / 2;  // stages per tile
+    constexpr int NS = S_NS;
+    constexpr int M = TILE_R / 16;
+    constexpr int N = 2;
+    constexpr int RB = KSTEPS * 64;  // row stride in bytes
+    constexpr int64_t TILE_BYTES = (int64_t)TILE_R * RB;
+    static_assert(SPT >= NS - 1, "prefetch distance must stay within the next tile");
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int qtile, split;
+    map_block(blockIdx.x, p, qtile, split);
+    if (qtile >= p.n_qtiles) return;
+    const int ct0 = (int)((int64_t)split * p.n_ctiles / p.splits);
+    const int ct1 = (int)((int64_t)(split + 1) * p.n_ctiles / p.splits);
+    const int ntiles = ct1 - ct0;
+    const int64_t q0 = (int64_t)qtile * TILE_Q;
+    if (p.trace && tid == 0) trace_block_start(p, qtile, split);
+
+    float* lst_d = (float*)(smem + S_LD_OFF);
+    int* lst_i = (int*)(smem + S_LI_OFF);
+    int* cnt = (int*)(smem + S_CNT_OFF);
+    float* tau = (float*)(smem + S_TAU_OFF);
+    const int qw0 = wave * 32;  // this wave's queries (tile-local)
+    if (lane < 32) {
+        cnt[qw0 + lane] = 0;
+        tau[qw0 + lane] = KEY_MAX;
+    }
+    unsigned* gtq = p.gtau + q0 + qw0;
+
+    // queries -> AGPRs (B fragments), settled once before the DMA ring starts
+    bfrag_t b[KSTEPS][N];
+    {
+        const char* qb = p.qop + (q0 + qw0 + (lane & 15)) * RB + (lane >> 4) * 16;
+#pragma unroll
+        for (int ks = 0; ks < KSTEPS; ++ks)
+#pragma unroll
+            for (int n = 0; n < N; ++n) b[ks][n] = *(const bfrag_t*)(qb + n * 16 * RB + ks * 64);
+#pragma unroll
+        for (int ks = 0; ks < KSTEPS; ++ks)
+#pragma unroll
+            for (int n = 0; n < N; ++n) AsmMmaV<DT>::settle(b[ks][n]);
+    }
+
+    // ---- DMA addressing: scalar tile bases, fixed per-lane offsets ----------
+    // piece jj of a wave = LDS block (wave*4 + jj) = 16-row block 2*wave + jj/2,
+    // 64-B half jj%2 of the stage's 128 B (fragment-ordered image)
+    const uint32_t voffA = (uint32_t)((2 * wave * 16 + (lane & 15)) * RB + (lane >> 4) * 16);
+    const uint32_t voffB = voffA + 16 * RB;
+    const uint32_t lds_base = lds_off(smem);
+    const uint32_t m0w = lds_base + S_RING_OFF + wave * 4096;
+    const uint32_t nslot_w = lds_base + S_NORM_OFF + wave * 256;
+    const char* cb_cur = p.codes + (int64_t)ct0 * TILE_BYTES;
+    const char* cb_nxt = ntiles > 1 ? cb_cur + TILE_BYTES : cb_cur;
+    const int nstep = lane < 8 ? TILE_R * 4 : 0;
+    const char* nv_cur = lane < 8 ? (const char*)(p.norms + (int64_t)ct0 * TILE_R + qw0 + lane * 4)
+                                  : (const char*)(gtq + ((lane - 8) & 7) * 4);
+    const char* nv_nxt = ntiles > 1 ? nv_cur + nstep : nv_cur;
+
+    // the 5 VMEM pieces of stage (t + NXT, JP) into ring slot `slot`
+    auto piece = [&](auto W, auto JP, auto NXT, uint32_t slot, int tnext) {
+        constexpr int w = decltype(W)::value, jp = decltype(JP)::value;
+        const char* cb = decltype(NXT)::value ? cb_nxt : cb_cur;
+        const uint32_t m0 = m0w + slot * S_STAGE + w * 1024;
+        if constexpr (w == 0) dma_piece<jp * STAGE_B>(voffA, cb, m0);
+        if constexpr (w == 1) dma_piece<jp * STAGE_B + 64>(voffA, cb, m0);
+        if constexpr (w == 2) dma_piece<jp * STAGE_B>(voffB, cb, m0);
+        if constexpr (w == 3) dma_piece<jp * STAGE_B + 64>(voffB, cb, m0);
+        if constexpr (w == 4)
+            dma_norm_piece(decltype(NXT)::value ? nv_nxt : nv_cur, nslot_w + (uint32_t)(tnext & 3) * S_NSLOT_B);
+    };
+
+    // prologue: stages 0 .. NS-2 (all in tile 0: SPT >= NS - 1)
+    static_for<NS - 1>([&](auto ST) {
+        constexpr int st = decltype(ST)::value;
+        static_for<5>([&](auto W) { piece(W, ST, std::false_type{}, (uint32_t)st, 0); });
+        (void)st;
+    });
+
+    // operand and accumulator registers: defined once, then only written by
+    // the pinned LDS reads / MFMAs below
+    f32x4 acc[M][N];
+    frag_t X[M], Y[M];
+    f32x4 yin[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+        acc[m][0] = acc[m][1] = yin[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+        X[m] = Y[m] = frag_t{};
+    }
+    const int rl0 = 4 * (lane >> 4);
+    int qloc[N];
+#pragma unroll
+    for (int n = 0; n < N; ++n) qloc[n] = qw0 + n * 16 + (lane & 15);
+    const bool qv0 = q0 + qloc[0] < p.nq, qv1 = q0 + qloc[1] < p.nq;
+    // per-lane LDS addresses: tau of my two queries, my thresholds in a norm slot
+    const uint32_t tau_addr = lds_off(tau + qloc[0]);
+    const uint32_t gt_lane = (uint32_t)(128 + (lane & 15) * 4);
+    const uint32_t nrm_lane = (uint32_t)(rl0 * 4);
+
+    asm volatile("s_waitcnt vmcnt(15)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    uint32_t rd_addr = lds_base + S_RING_OFF + (uint32_t)lane * 16;  // slot 0
+    if (ntiles > 0) {
+        static_for<M>([&](auto MM) {
+            constexpr int m = decltype(MM)::value;
+            ds_rd128<m * 2048>(X[m], rd_addr);
+        });
+        // row norms of tile 0 (rows rl0 + 16 m .. +3): [wave w][row%32] layout
+        const uint32_t na = lds_base + S_NORM_OFF + nrm_lane;
+        static_for<M>([&](auto MM) {
+            constexpr int m = decltype(MM)::value;
+            ds_rd128<(m >> 1) * 256 + (m & 1) * 64>(yin[m], na);
+        });
+    }
+
+    int c = 0;  // ring slot of the current stage
+    for (int t = 0; t < ntiles; ++t) {
+        float tr[N];
+        unsigned gr[N];
+        static_for<SPT>([&](auto JJ) {
+            constexpr int j = decltype(JJ)::value;
+            constexpr bool LAST = j == SPT - 1;
+            constexpr int jp = (j + NS - 1) % SPT;  // stage issued now: (t + nxt, jp)
+            constexpr bool nxt = j + NS - 1 >= SPT;
+            typedef std::integral_constant<bool, nxt> NXT;
+            typedef std::integral_constant<int, jp> JP;
+            const uint32_t c1 = c == NS - 1 ? 0u : (uint32_t)c + 1;  // slot of stage g+1
+            const uint32_t c4 = c == 0 ? (uint32_t)NS - 1 : (uint32_t)c - 1;  // slot of stage g+NS-1
+            const int tnext = t + (nxt ? 1 : 0);
+            // stage g+1 landed for every wave; X (half 0 of stage g) is in registers;
+            // slot c4 is no longer read by anyone
+            asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            // ---- half 0: X MFMAs; read half 1 (Y) of this stage meanwhile
+            static_for<M>([&](auto MM) {
+                constexpr int m = decltype(MM)::value;
+                constexpr int INIT = j == 0 ? (METRIC == L2 ? 1 : 2) : 0;
+                AsmMmaV<DT>::template mma2<INIT>(acc[m][0], acc[m][1], X[m], b[2 * j][0], b[2 * j][1], yin[m]);
+                ds_rd128<m * 2048 + 1024>(Y[m], rd_addr);
+                if constexpr (m == 2) piece(std::integral_constant<int, 0>{}, JP{}, NXT{}, c4, tnext);
+                if constexpr (m == 5) piece(std::integral_constant<int, 1>{}, JP{}, NXT{}, c4, tnext);
+            });
+            if constexpr (LAST) {
+                // epilogue operands of this tile (thresholds) and the next
+                // tile's row norms (its first MFMAs' srcC)
+                ds_rd32<0>(tr[0], tau_addr);
+                ds_rd32<64>(tr[1], tau_addr);
+                const uint32_t ns = lds_base + S_NORM_OFF + (uint32_t)(t & 3) * S_NSLOT_B + wave * 256 + gt_lane;
+                ds_rd32<0>(gr[0], ns);
+                ds_rd32<64>(gr[1], ns);
+                const uint32_t na = lds_base + S_NORM_OFF + (uint32_t)((t + 1) & 3) * S_NSLOT_B + nrm_lane;
+                static_for<M>([&](auto MM) {
+                    constexpr int m = decltype(MM)::value;
+                    ds_rd128<(m >> 1) * 256 + (m & 1) * 64>(yin[m], na);
+                });
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            // ---- half 1: Y MFMAs; read half 0 (X) of stage g+1 meanwhile
+            const uint32_t rd_next = lds_base + S_RING_OFF + c1 * S_STAGE + (uint32_t)lane * 16;
+            static_for<M>([&](auto MM) {
+                constexpr int m = decltype(MM)::value;
+                AsmMmaV<DT>::template mma2<0>(acc[m][0], acc[m][1], Y[m], b[2 * j + 1][0], b[2 * j + 1][1], yin[m]);
+                if constexpr (m >= 1) ds_rd128<(m - 1) * 2048>(X[m - 1], rd_next);
+                if constexpr (m == 1) piece(std::integral_constant<int, 2>{}, JP{}, NXT{}, c4, tnext);
+                if constexpr (m == 3) piece(std::integral_constant<int, 3>{}, JP{}, NXT{}, c4, tnext);
+                if constexpr (m == 5) piece(std::integral_constant<int, 4>{}, JP{}, NXT{}, c4, tnext);
+            });
+            ds_rd128<(M - 1) * 2048>(X[M - 1], rd_next);
+            __builtin_amdgcn_sched_barrier(0);
+            rd_addr = rd_next;
+            c = (int)c1;
+        });
+
+        // ---- epilogue of tile t: the accumulator holds the keys ------------
+        acc_fence_v(acc);
+        if (p.dbgbuf) {  // diagnostics (FX_SCAN_DBG & 32): every key -> [nq_pad][cap rows]
+            float* keys = (float*)p.dbgbuf;
+            const int64_t ld = (int64_t)p.n_ctiles * TILE_R;
+#pragma unroll
+            for (int n = 0; n < N; ++n)
+#pragma unroll
+                for (int m = 0; m < M; ++m)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        keys[(q0 + qloc[n]) * ld + (int64_t)(ct0 + t) * TILE_R + rl0 + 16 * m + i] = acc[m][n][i];
+        }
+        float tn[N];
+        tn[0] = qv0 ? fminf(tr[0], ord2f(gr[0])) : -FX_INF;
+        tn[1] = qv1 ? fminf(tr[1], ord2f(gr[1])) : -FX_INF;
+        float gmin[N][M], mn[N];
+#pragma unroll
+        for (int n = 0; n < N; ++n) {
+#pragma unroll
+            for (int m = 0; m < M; ++m)
+                gmin[n][m] = fminf(fminf(acc[m][n][0], acc[m][n][1]), fminf(acc[m][n][2], acc[m][n][3]));
+            mn[n] = gmin[n][0];
+#pragma unroll
+            for (int m = 1; m < M; ++m) mn[n] = fminf(mn[n], gmin[n][m]);
+        }
+        if (__builtin_amdgcn_ballot_w64(mn[0] <= tn[0] || mn[1] <= tn[1])) {
+            // slow path: some row beats a query's threshold
+            const int trow0 = (ct0 + t) * TILE_R;
+            const int rlim = p.ntotal < (int64_t)trow0 + TILE_R ? (int)p.ntotal : trow0 + TILE_R;
+            unsigned pend[N] = {0u, 0u};
+            bool ovf = false;
+            static_for<N>([&](auto NN) {
+                constexpr int n = decltype(NN)::value;
+                if (__builtin_amdgcn_ballot_w64(mn[n] <= tn[n])) {
+                    static_for<M>([&](auto MM) {
+                        constexpr int m = decltype(MM)::value;
+                        if (__builtin_amdgcn_ballot_w64(gmin[n][m] <= tn[n]))
+                            ovf |= push_group<M, N>(acc, n, m, 15u, tn[n], qloc[n], trow0 + rl0 + m * 16, rlim,
+                                                    lst_d, lst_i, cnt, pend[n]);
+                    });
+                }
+            });
+            while (__builtin_amdgcn_ballot_w64(ovf)) {
+                compact_wave(lst_d, lst_i, cnt, tau, gtq, qw0, lane);
+                ovf = false;
+                static_for<N>([&](auto NN) {
+                    constexpr int n = decltype(NN)::value;
+                    const float tq = (n == 0 ? qv0 : qv1) ? fminf(tau[qloc[n]], tn[n]) : -FX_INF;
+                    const unsigned pn = pend[n];
+                    pend[n] = 0u;
+                    static_for<M>([&](auto MM) {
+                        constexpr int m = decltype(MM)::value;
+                        const unsigned el = (pn >> (4 * m)) & 15u;
+                        if (__builtin_amdgcn_ballot_w64(el != 0u))
+                            ovf |= push_group<M, N>(acc, n, m, el, tq, qloc[n], trow0 + rl0 + m * 16, rlim, lst_d,
+                                                    lst_i, cnt, pend[n]);
+                    });
+                });
+            }
+        }
+        // advance the tile bases (clamped: stages past the end re-read the last tile)
+        cb_cur = cb_nxt;
+        nv_cur = nv_nxt;
+        if (t + 2 < ntiles) {
+            cb_nxt += TILE_BYTES;
+            nv_nxt += nstep;
+        }
+    }
+
+    // retire the ring's look-ahead pieces: an LDS-DMA still in flight at exit
+    // would land in the LDS of the next workgroup on this CU
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // final flush: sorted top-KP per query of this (query tile, split)
+    const int64_t obase = ((int64_t)qtile * p.splits + split) * TILE_Q;
+    for (int qi = 0; qi < 32; ++qi) {
+        const int q = qw0 + qi;
+        if (q0 + q >= p.nq) break;
+        const int cn = min(cnt[q], CAP);
+        float d = lane < cn ? lst_d[q * CAP + lane] : FX_INF;
+        int i = lane < cn ? lst_i[q * CAP + lane] : INT_MAX;
+        sort64(d, i, lane);
+        if (lane < KP) {
+            p.cand_d[(obase + q) * KP + lane] = d;
+            p.cand_i[(obase + q) * KP + lane] = i == INT_MAX ? -1 : i;
+        }
+    }
+    if (p.trace && tid == 0) p.trace[blockIdx.x * 4 + 3] = wall_clock64();
+}
+
+template <int DT, int METRIC, int KSTEPS>
+static hipError_t scan_v4_t(const ScanParams& p, hipStream_t s) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_scan_v4<DT, METRIC, KSTEPS>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, S_LDS_BYTES);
+    if (e != hipSuccess) return e;
+    const int grid = p.qt_per_xcd > 0 ? 8 * p.qt_per_xcd * p.splits : p.n_qtiles * p.splits;
+    hipLaunchKernelGGL((k_scan_v4<DT, METRIC, KSTEPS>), dim3(grid), dim3(SCAN_THREADS), S_LDS_BYTES, s, p);
+    return hipGetLastError();
+}
+
+template <int DT, int METRIC>
+static hipError_t scan_rows(const ScanParams& p, hipStream_t s, bool* handled) {
+    *handled = true;
+    switch (p.row_bytes / 64) {
+        case 8: return scan_v4_t<DT, METRIC, 8>(p, s);
+        case 12: return scan_v4_t<DT, METRIC, 12>(p, s);
+        case 16: return scan_v4_t<DT, METRIC, 16>(p, s);
+        case 24: return scan_v4_t<DT, METRIC, 24>(p, s);
+        default: *handled = false; return hipSuccess;
+    }
+}
+
+hipError_t launch_scan_mfma(int st_dt, int metric, const ScanParams& p, hipStream_t s, bool* handled) {
+    if (p.row_bytes % 64 != 0) {
+        *handled = false;
+        return hipSuccess;
+    }
+    if (metric == L2) {
+        if (st_dt == F32) return scan_rows<F32, L2>(p, s, handled);
+        if (st_dt == BF16) return scan_rows<BF16, L2>(p, s, handled);
+        return scan_rows<F16, L2>(p, s, handled);
+    }
+    if (st_dt == F32) return scan_rows<F32, IP>(p, s, handled);
+    if (st_dt == BF16) return scan_rows<BF16, IP>(p, s, handled);
+    return scan_rows<F16, IP>(p, s, handled);
+}
+
+}  // namespace fx

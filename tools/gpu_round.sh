@@ -1,0 +1,12 @@
+#!/bin/bash
+# One GPU-box session: parity tests, the default bench line, a placement trace
+# of the scan, and the rocprofv3 evidence.  Every GPU step has its own time
+# limit and the steps stop at the first failure.
+set -euo pipefail
+out=gpurun_out/${1:-r1}
+mkdir -p "$out"
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$out/pytest.log" 2>&1
+timeout -k 10 300 python -u bench.py > "$out/bench.json" 2> "$out/bench.err"
+FX_SCAN_TRACE="$out/scan_trace.bin" timeout -k 10 200 python -u bench.py --no-cpu --steps 1 --warmup 1 > "$out/trace_bench.json" 2>&1
+python tools/analyze_trace.py "$out/scan_trace.bin" > "$out/trace.txt" 2>&1 || true
+echo done

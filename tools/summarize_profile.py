@@ -20,7 +20,7 @@ from collections import defaultdict
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-SCAN = "k_scan_qreg"
+SCAN = "k_scan_v4"
 
 
 def counters(path):

@@ -76,6 +76,14 @@ __device__ __forceinline__ void dma_piece(uint32_t voff, const char* sbase, uint
                  "{m0}"(lds - OFF)
                  : "memory");
 }
+// a wave-uniform pointer, asserted so (the "s" operand of dma_piece needs it in
+// an SGPR pair; hipcc's divergence analysis does not always prove it)
+__device__ __forceinline__ const char* sgpr_ptr(const char* p) {
+    const uint64_t v = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (const char*)(((uint64_t)hi << 32) | lo);
+}
 // the per-stage row-norm / threshold piece: lanes 0-7 move 32 row norms,
 // lanes 8-15 the wave's 32 shared thresholds; lanes 16-63 are masked off
 __device__ __forceinline__ void dma_norm_piece(const char* vaddr, uint32_t m0) {
@@ -151,7 +159,11 @@ __device__ __forceinline__ bool push_group(const f32x4 (&acc)[M][N], int n, int 
     return ovf;
 }
 
-template <int DT, int METRIC, int KSTEPS>
+// ABL: compile-time ablation switches of profiling builds (FX_ABLATION; 0 in
+// the product): 1 L2-resident corpus, 2 no corpus DMA, 4 no MFMA, 8 no
+// epilogue, 16 no per-stage barrier, 32 no mid-stage LDS wait -- timing only,
+// results invalid
+template <int DT, int METRIC, int KSTEPS, int ABL = 0>
 __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     typedef typename AsmMmaV<DT>::A frag_t;
@@ -208,8 +220,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
     const uint32_t lds_base = lds_off(smem);
     const uint32_t m0w = lds_base + S_RING_OFF + wave * 4096;
     const uint32_t nslot_w = lds_base + S_NORM_OFF + wave * 256;
-    const char* cb_cur = p.codes + (int64_t)ct0 * TILE_BYTES;
-    const char* cb_nxt = ntiles > 1 ? cb_cur + TILE_BYTES : cb_cur;
+    const char* cb_cur = sgpr_ptr(p.codes + (int64_t)ct0 * TILE_BYTES);
+    const char* cb_nxt = sgpr_ptr(ntiles > 1 ? cb_cur + TILE_BYTES : cb_cur);
     const int nstep = lane < 8 ? TILE_R * 4 : 0;
     const char* nv_cur = lane < 8 ? (const char*)(p.norms + (int64_t)ct0 * TILE_R + qw0 + lane * 4)
                                   : (const char*)(gtq + ((lane - 8) & 7) * 4);
@@ -220,6 +232,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
         constexpr int w = decltype(W)::value, jp = decltype(JP)::value;
         const char* cb = decltype(NXT)::value ? cb_nxt : cb_cur;
         const uint32_t m0 = m0w + slot * S_STAGE + w * 1024;
+        if constexpr (w < 4 && (ABL & 2)) return;  // ablation: no corpus DMA (results invalid)
         if constexpr (w == 0) dma_piece<jp * STAGE_B>(voffA, cb, m0);
         if constexpr (w == 1) dma_piece<jp * STAGE_B + 64>(voffA, cb, m0);
         if constexpr (w == 2) dma_piece<jp * STAGE_B>(voffB, cb, m0);
@@ -287,44 +300,59 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
             const int tnext = t + (nxt ? 1 : 0);
             // stage g+1 landed for every wave; X (half 0 of stage g) is in registers;
             // slot c4 is no longer read by anyone
-            asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            if constexpr (ABL & 16)
+                asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)" ::: "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)\n\ts_barrier" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
             // ---- half 0: X MFMAs; read half 1 (Y) of this stage meanwhile
             static_for<M>([&](auto MM) {
                 constexpr int m = decltype(MM)::value;
                 constexpr int INIT = j == 0 ? (METRIC == L2 ? 1 : 2) : 0;
-                AsmMmaV<DT>::template mma2<INIT>(acc[m][0], acc[m][1], X[m], b[2 * j][0], b[2 * j][1], yin[m]);
-                ds_rd128<m * 2048 + 1024>(Y[m], rd_addr);
-                if constexpr (m == 2) piece(std::integral_constant<int, 0>{}, JP{}, NXT{}, c4, tnext);
-                if constexpr (m == 5) piece(std::integral_constant<int, 1>{}, JP{}, NXT{}, c4, tnext);
+                if constexpr (!(ABL & 4))
+                    AsmMmaV<DT>::template mma2<INIT>(acc[m][0], acc[m][1], X[m], b[2 * j][0], b[2 * j][1], yin[m]);
+                // half 1 of this stage: two reads per pair over the first four
+                // pairs, so the mid-stage wait finds them landed
+                if constexpr (m < M / 2) {
+                    ds_rd128<(2 * m) * 2048 + 1024>(Y[2 * m], rd_addr);
+                    ds_rd128<(2 * m + 1) * 2048 + 1024>(Y[2 * m + 1], rd_addr);
+                }
+                if constexpr (LAST && m >= M / 2) {
+                    // the next tile's row norms (its first MFMAs' srcC)
+                    const uint32_t na = lds_base + S_NORM_OFF + (uint32_t)((t + 1) & 3) * S_NSLOT_B + nrm_lane;
+                    constexpr int m0 = 2 * (m - M / 2), m1 = m0 + 1;
+                    ds_rd128<(m0 >> 1) * 256 + (m0 & 1) * 64>(yin[m0], na);
+                    ds_rd128<(m1 >> 1) * 256 + (m1 & 1) * 64>(yin[m1], na);
+                }
+                if constexpr (m == 4) piece(std::integral_constant<int, 0>{}, JP{}, NXT{}, c4, tnext);
+                if constexpr (m == 6) piece(std::integral_constant<int, 1>{}, JP{}, NXT{}, c4, tnext);
             });
             if constexpr (LAST) {
-                // epilogue operands of this tile (thresholds) and the next
-                // tile's row norms (its first MFMAs' srcC)
+                // epilogue operands of this tile: the queries' thresholds
                 ds_rd32<0>(tr[0], tau_addr);
                 ds_rd32<64>(tr[1], tau_addr);
                 const uint32_t ns = lds_base + S_NORM_OFF + (uint32_t)(t & 3) * S_NSLOT_B + wave * 256 + gt_lane;
                 ds_rd32<0>(gr[0], ns);
                 ds_rd32<64>(gr[1], ns);
-                const uint32_t na = lds_base + S_NORM_OFF + (uint32_t)((t + 1) & 3) * S_NSLOT_B + nrm_lane;
-                static_for<M>([&](auto MM) {
-                    constexpr int m = decltype(MM)::value;
-                    ds_rd128<(m >> 1) * 256 + (m & 1) * 64>(yin[m], na);
-                });
             }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if constexpr (!(ABL & 32)) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
             // ---- half 1: Y MFMAs; read half 0 (X) of stage g+1 meanwhile
             const uint32_t rd_next = lds_base + S_RING_OFF + c1 * S_STAGE + (uint32_t)lane * 16;
             static_for<M>([&](auto MM) {
                 constexpr int m = decltype(MM)::value;
-                AsmMmaV<DT>::template mma2<0>(acc[m][0], acc[m][1], Y[m], b[2 * j + 1][0], b[2 * j + 1][1], yin[m]);
-                if constexpr (m >= 1) ds_rd128<(m - 1) * 2048>(X[m - 1], rd_next);
-                if constexpr (m == 1) piece(std::integral_constant<int, 2>{}, JP{}, NXT{}, c4, tnext);
-                if constexpr (m == 3) piece(std::integral_constant<int, 3>{}, JP{}, NXT{}, c4, tnext);
-                if constexpr (m == 5) piece(std::integral_constant<int, 4>{}, JP{}, NXT{}, c4, tnext);
+                if constexpr (!(ABL & 4))
+                    AsmMmaV<DT>::template mma2<0>(acc[m][0], acc[m][1], Y[m], b[2 * j + 1][0], b[2 * j + 1][1], yin[m]);
+                // half 0 of stage g+1: two reads per pair over the first four
+                // pairs (X[2m+1]'s last reader is >= 8 MFMAs back)
+                if constexpr (m < M / 2) {
+                    ds_rd128<(2 * m) * 2048>(X[2 * m], rd_next);
+                    ds_rd128<(2 * m + 1) * 2048>(X[2 * m + 1], rd_next);
+                }
+                if constexpr (m == 4) piece(std::integral_constant<int, 2>{}, JP{}, NXT{}, c4, tnext);
+                if constexpr (m == 5) piece(std::integral_constant<int, 3>{}, JP{}, NXT{}, c4, tnext);
+                if constexpr (m == 6) piece(std::integral_constant<int, 4>{}, JP{}, NXT{}, c4, tnext);
             });
-            ds_rd128<(M - 1) * 2048>(X[M - 1], rd_next);
             __builtin_amdgcn_sched_barrier(0);
             rd_addr = rd_next;
             c = (int)c1;
@@ -356,7 +384,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
 #pragma unroll
             for (int m = 1; m < M; ++m) mn[n] = fminf(mn[n], gmin[n][m]);
         }
-        if (__builtin_amdgcn_ballot_w64(mn[0] <= tn[0] || mn[1] <= tn[1])) {
+        if (!(ABL & 8) && __builtin_amdgcn_ballot_w64(mn[0] <= tn[0] || mn[1] <= tn[1])) {
             // slow path: some row beats a query's threshold
             const int trow0 = (ct0 + t) * TILE_R;
             const int rlim = p.ntotal < (int64_t)trow0 + TILE_R ? (int)p.ntotal : trow0 + TILE_R;
@@ -392,11 +420,16 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
             }
         }
         // advance the tile bases (clamped: stages past the end re-read the last tile)
-        cb_cur = cb_nxt;
+        cb_cur = sgpr_ptr(cb_nxt);
         nv_cur = nv_nxt;
         if (t + 2 < ntiles) {
             cb_nxt += TILE_BYTES;
             nv_nxt += nstep;
+            if ((ABL & 1) && ((t + 2) & 7) == 0) {  // ablation: L2-resident corpus (8 tiles), results invalid
+                cb_nxt -= 8 * TILE_BYTES;
+                nv_nxt -= 8 * nstep;
+            }
+            cb_nxt = sgpr_ptr(cb_nxt);
         }
     }
 
@@ -420,13 +453,30 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
     if (p.trace && tid == 0) p.trace[blockIdx.x * 4 + 3] = wall_clock64();
 }
 
-template <int DT, int METRIC, int KSTEPS>
+template <int DT, int METRIC, int KSTEPS, int ABL = 0>
 static hipError_t scan_v4_t(const ScanParams& p, hipStream_t s) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_scan_v4<DT, METRIC, KSTEPS>,
+#ifdef FX_ABLATION
+    if constexpr (ABL == 0 && DT == BF16 && METRIC == L2 && KSTEPS == 24) {
+        switch (p.dbg & 63) {
+            case 1: return scan_v4_t<DT, METRIC, KSTEPS, 1>(p, s);
+            case 2: return scan_v4_t<DT, METRIC, KSTEPS, 2>(p, s);
+            case 4: return scan_v4_t<DT, METRIC, KSTEPS, 4>(p, s);
+            case 8: return scan_v4_t<DT, METRIC, KSTEPS, 8>(p, s);
+            case 10: return scan_v4_t<DT, METRIC, KSTEPS, 10>(p, s);
+            case 14: return scan_v4_t<DT, METRIC, KSTEPS, 14>(p, s);
+            case 26: return scan_v4_t<DT, METRIC, KSTEPS, 26>(p, s);
+            case 42: return scan_v4_t<DT, METRIC, KSTEPS, 42>(p, s);
+            case 58: return scan_v4_t<DT, METRIC, KSTEPS, 58>(p, s);
+            case 16: return scan_v4_t<DT, METRIC, KSTEPS, 16>(p, s);
+            default: break;
+        }
+    }
+#endif
+    hipError_t e = hipFuncSetAttribute((const void*)k_scan_v4<DT, METRIC, KSTEPS, ABL>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, S_LDS_BYTES);
     if (e != hipSuccess) return e;
     const int grid = p.qt_per_xcd > 0 ? 8 * p.qt_per_xcd * p.splits : p.n_qtiles * p.splits;
-    hipLaunchKernelGGL((k_scan_v4<DT, METRIC, KSTEPS>), dim3(grid), dim3(SCAN_THREADS), S_LDS_BYTES, s, p);
+    hipLaunchKernelGGL((k_scan_v4<DT, METRIC, KSTEPS, ABL>), dim3(grid), dim3(SCAN_THREADS), S_LDS_BYTES, s, p);
     return hipGetLastError();
 }
 

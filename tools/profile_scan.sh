@@ -17,6 +17,6 @@ timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$out/write"
     python3 bench.py --no-cpu "$@" > "$out/write.log" 2>&1
 timeout -k 10 400 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$out/tcc" -o run -- \
     python3 bench.py --no-cpu "$@" > "$out/tcc.log" 2>&1
-timeout -k 10 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE \
+timeout -k 10 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE \
     --output-format csv -d "$out/sq" -o run -- python3 bench.py --no-cpu "$@" > "$out/sq.log" 2>&1
 echo "profile $tag done"

@@ -22,7 +22,9 @@ typedef __attribute__((__vector_size__(4 * sizeof(float)))) float f32x4;
 constexpr int NSLOT = 5;
 constexpr int STAGE = 16384;
 constexpr size_t BUF = 4ull << 30;
-constexpr size_t WIN = 16ull << 20;
+static size_t WIN_H = 16ull << 20;  // per-block streamed window (host-set)
+__constant__ size_t WIN;
+__constant__ int NWIN;  // stages per window
 constexpr int ROWB = 1536;
 
 __device__ __forceinline__ uint32_t lds_off(const void* p) {
@@ -48,23 +50,30 @@ __global__ __launch_bounds__(NW * 64, 1) void probe(const char* buf, int nstage,
         for (int i = 0; i < 8; ++i)
             for (int j = 0; j < 8; ++j) a[s][i][j] = (__bf16)(0.001f * (lane * 3 + i + j + s));
 
+    // per-lane offsets of this wave's pieces inside a stage (fragment-ordered
+    // image as in fx_scan.hip), scalar stage base: no vector address math
+    uint32_t voff[4];
+    for (int p = 0; p < 4; ++p) {
+        const int piece = wave * NDMA + p;
+        voff[p] = CONTIG ? (uint32_t)(piece * 1024 + lane * 16)
+                         : (uint32_t)((((piece >> 1) & 7) * 16 + (lane & 15)) * ROWB + (piece & 1) * 64 +
+                                      (lane >> 4) * 16);
+    }
     auto dma = [&](int g, int p) {
         if (NODMA) return;
         const int piece = wave * NDMA + p;  // 0..15 per stage per CU
-        size_t off;
-        if (CONTIG) {
-            off = ((size_t)g * STAGE + piece * 1024 + lane * 16) % WIN;
-        } else {
-            const size_t row = (size_t)g * 128 + (piece >> 1) * 16 + (lane & 15);
-            off = (row * ROWB + (piece & 1) * 64 + (lane >> 4) * 16) % WIN;
-        }
-        const uint32_t m0 = lbase + (g % NSLOT) * STAGE + piece * 1024;
-        asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(win + off),
+        const uint64_t b = (uint64_t)(win + (size_t)(g % NWIN) * (CONTIG ? STAGE : 128 * ROWB));
+        // readfirstlane returns int: go through uint32_t (no sign extension)
+        const uint32_t bhi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+        const uint32_t blo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
+        const char* sb = (const char*)(((uint64_t)bhi << 32) | blo);
+        const uint32_t m0 = lbase + 4096 + (g % NSLOT) * STAGE + piece * 1024;
+        asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff[p]), "s"(sb),
                      "{m0}"(__builtin_amdgcn_readfirstlane(m0))
                      : "memory");
     };
     auto rd = [&](int g, bf16x8(&d)[8], int half) {
-        const uint32_t base = lbase + (g % NSLOT) * STAGE + lane * 16 + half * 1024;
+        const uint32_t base = lbase + 4096 + (g % NSLOT) * STAGE + lane * 16 + half * 1024;
         asm volatile(
             "ds_read_b128 %0, %8\n\t"
             "ds_read_b128 %1, %8 offset:2048\n\t"
@@ -147,7 +156,11 @@ void run(const char* name, const char* buf, int nstage) {
     double best = 1e30, clk = 0;
     for (int rep = 0; rep < 4; ++rep) {
         hipLaunchKernelGGL(k, dim3(grid), dim3(NW * 64), 150000, 0, buf, nstage, d);
-        hipDeviceSynchronize();
+        hipError_t e0 = hipGetLastError(), e1 = hipDeviceSynchronize();
+        if (e0 != hipSuccess || e1 != hipSuccess) {
+            printf("%s: launch %s / sync %s\n", name, hipGetErrorString(e0), hipGetErrorString(e1));
+            exit(1);
+        }
         hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost);
         std::vector<double> cyc, ghz;
         for (int i = 0; i < grid * NW; ++i) {
@@ -169,6 +182,11 @@ void run(const char* name, const char* buf, int nstage) {
 
 int main(int argc, char** argv) {
     int nstage = argc > 1 ? atoi(argv[1]) : 4000;
+    WIN_H = (argc > 2 ? (size_t)atoll(argv[2]) : 16) << 10;  // KiB
+    hipMemcpyToSymbol(HIP_SYMBOL(WIN), &WIN_H, sizeof(WIN_H));
+    const int nwin = (int)std::max<size_t>(1, WIN_H / (128 * ROWB));
+    hipMemcpyToSymbol(HIP_SYMBOL(NWIN), &nwin, sizeof(nwin));
+    printf("window per block: %zu KiB\n", WIN_H >> 10);
     char* buf;
     hipMalloc(&buf, BUF);
     hipMemset(buf, 0x3c, BUF);

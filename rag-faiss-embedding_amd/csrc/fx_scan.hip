@@ -16,9 +16,11 @@
 //     stage with a scalar base (SGPR pair) + fixed per-lane offsets, so a
 //     piece costs one SALU add for M0 and no vector address arithmetic;
 //     the fragment-ordered LDS image makes every ds_read_b128 contiguous;
-//   * one counted `s_waitcnt vmcnt(10)` + s_barrier per stage (exactly 5 VMEM
-//     ops per wave per stage: 4 corpus pieces + 1 row-norm / shared-threshold
-//     piece), no other VMEM in the loop;
+//   * one counted `s_waitcnt vmcnt(N_j)` + s_barrier per stage: each wave
+//     issues 4 corpus pieces per stage, plus one row-norm / shared-threshold
+//     piece with the prefetch of each tile's first stage; N_j is the
+//     compile-time count issued after the stage the barrier retires; no other
+//     VMEM in the loop;
 //   * A fragments double-buffered in two register sets: half 1 of stage g is
 //     read during half 0's MFMAs, half 0 of stage g+1 during half 1's MFMAs;
 //   * a tile's first MFMA takes srcC = |y|^2 of its rows (L2), so after the
@@ -244,7 +246,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
     // prologue: stages 0 .. NS-2 (all in tile 0: SPT >= NS - 1)
     static_for<NS - 1>([&](auto ST) {
         constexpr int st = decltype(ST)::value;
-        static_for<5>([&](auto W) { piece(W, ST, std::false_type{}, (uint32_t)st, 0); });
+        static_for<4>([&](auto W) { piece(W, ST, std::false_type{}, (uint32_t)st, 0); });
+        if constexpr (st == 0) piece(std::integral_constant<int, 4>{}, ST, std::false_type{}, 0u, 0);
         (void)st;
     });
 
@@ -268,7 +271,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
     const uint32_t gt_lane = (uint32_t)(128 + (lane & 15) * 4);
     const uint32_t nrm_lane = (uint32_t)(rl0 * 4);
 
-    asm volatile("s_waitcnt vmcnt(15)\n\ts_barrier" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");  // stage 0 (5 pieces) landed
     __builtin_amdgcn_sched_barrier(0);
     uint32_t rd_addr = lds_base + S_RING_OFF + (uint32_t)lane * 16;  // slot 0
     if (ntiles > 0) {
@@ -300,10 +303,14 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
             const int tnext = t + (nxt ? 1 : 0);
             // stage g+1 landed for every wave; X (half 0 of stage g) is in registers;
             // slot c4 is no longer read by anyone
+            // VMEM ops younger than stage g+1's: those issued in stages g-2, g-1
+            // (4 corpus pieces each, + the norm piece where that stage
+            // prefetched a tile's first stage)
+            constexpr int W = 8 + ((j + 3) % SPT == 0) + ((j + 2) % SPT == 0);
             if constexpr (ABL & 16)
-                asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)" ::: "memory");
+                asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(W) : "memory");
             else
-                asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(W) : "memory");
             __builtin_amdgcn_sched_barrier(0);
             // ---- half 0: X MFMAs; read half 1 (Y) of this stage meanwhile
             static_for<M>([&](auto MM) {
@@ -351,7 +358,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                 }
                 if constexpr (m == 4) piece(std::integral_constant<int, 2>{}, JP{}, NXT{}, c4, tnext);
                 if constexpr (m == 5) piece(std::integral_constant<int, 3>{}, JP{}, NXT{}, c4, tnext);
-                if constexpr (m == 6) piece(std::integral_constant<int, 4>{}, JP{}, NXT{}, c4, tnext);
+                if constexpr (m == 6 && jp == 0) piece(std::integral_constant<int, 4>{}, JP{}, NXT{}, c4, tnext);
             });
             __builtin_amdgcn_sched_barrier(0);
             rd_addr = rd_next;

@@ -80,6 +80,8 @@ hipError_t launch_prep_queries(const void* q, int q_dt, int64_t nq, int64_t nq_p
 hipError_t launch_scan(int st_dt, int metric, const ScanParams& p, hipStream_t s);
 // fx_scan.hip: the MFMA scan; *handled = false when it has no kernel for p.row_bytes
 hipError_t launch_scan_mfma(int st_dt, int metric, const ScanParams& p, hipStream_t s, bool* handled);
+// fx_scan5.hip: the 8-wave K-split variant (selected by FX_SCAN_V5=1)
+hipError_t launch_scan_mfma5(int st_dt, int metric, const ScanParams& p, hipStream_t s, bool* handled);
 hipError_t launch_refine(int st_dt, int metric, const RefineParams& p, hipStream_t s);
 hipError_t launch_exact_fallback(int st_dt, int metric, const char* codes, int row_bytes, int kdim,
                                  int64_t ntotal, const float* qf32, const int* qlist, int nlist,

@@ -17,8 +17,8 @@
 //     ds_read_b128, 16 MFMAs (4 row blocks x 2 query columns x 2 K-steps);
 //   once per tile each wave also moves an aux piece (h = 1: 16 row norms of
 //     its row block; h = 0: its pair's 32 shared thresholds);
-//   epilogue: wave (p, h) finalises the 16 queries of column n = h: its own
-//     partial + the partner's (2 LDS rounds of 16 KiB) + |y|^2 (L2), then the
+//   epilogue: wave (p, h) finalises queries 32p + 16h .. +15 (its column 0):
+//     its own partial + the partner's (2 LDS rounds of 16 KiB) + |y|^2 (L2), then the
 //     group-ballot push of k_scan_v4 into its own 16 LDS lists.
 //
 // Not yet measured on hardware: selected only with FX_SCAN_V5=1 (the product
@@ -145,11 +145,14 @@ __global__ __launch_bounds__(V5_THREADS, 1) void k_scan_v5(ScanParams p) {
     // the pair's 32 queries, this wave's K half -> AGPRs
     bfrag_t b[KH][N];
     {
+        // column n holds queries pr*32 + (n ^ h)*16 ..: column 0 is always the
+        // 16 queries this wave finalises, column 1 its partner's (no dynamic
+        // register indexing in the epilogue)
         const char* qb = p.qop + (q0 + pr * 32 + (lane & 15)) * RB + h * HB + (lane >> 4) * 16;
 #pragma unroll
         for (int ks = 0; ks < KH; ++ks)
 #pragma unroll
-            for (int n = 0; n < N; ++n) b[ks][n] = *(const bfrag_t*)(qb + n * 16 * RB + ks * 64);
+            for (int n = 0; n < N; ++n) b[ks][n] = *(const bfrag_t*)(qb + (n ^ h) * 16 * RB + ks * 64);
 #pragma unroll
         for (int ks = 0; ks < KH; ++ks)
 #pragma unroll
@@ -219,7 +222,8 @@ __global__ __launch_bounds__(V5_THREADS, 1) void k_scan_v5(ScanParams p) {
     const bool qv = q0 + ql < p.nq;
     const uint32_t tau_addr = lds_off(tau + ql);
     const uint32_t gt_lane = (uint32_t)(256 + pr * 128 + h * 64 + (lane & 15) * 4);
-    // exchange: wave (pr, h) writes column 1-h for its partner, reads column h
+    // exchange: wave (pr, h) writes its column 1 (the partner's queries) into the
+    // partner's region and reads its own region
     const uint32_t xw = lds_base + V5_XCH_OFF + (uint32_t)(((pr * 2 + (1 - h)) * 2) * 1024 + lane * 16);
     const uint32_t xr = lds_base + V5_XCH_OFF + (uint32_t)(((pr * 2 + h) * 2) * 1024 + lane * 16);
     unsigned* gt_first = p.gtau + q0 + qf;
@@ -303,21 +307,21 @@ __global__ __launch_bounds__(V5_THREADS, 1) void k_scan_v5(ScanParams p) {
         // exchange the partner column in two rounds (m = 0,1 then 2,3)
         static_for<2>([&](auto RR) {
             constexpr int r = decltype(RR)::value;
-            ds_wr128<0>(xw, acc[2 * r][1 - h]);
-            ds_wr128<1024>(xw, acc[2 * r + 1][1 - h]);
+            ds_wr128<0>(xw, acc[2 * r][1]);
+            ds_wr128<1024>(xw, acc[2 * r + 1][1]);
             asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
             f32x4 o0, o1;
             asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:1024\n\ts_waitcnt lgkmcnt(0)"
                          : "=&v"(o0), "=&v"(o1)
                          : "v"(xr)
                          : "memory");
-            acc[2 * r][h] += o0;
-            acc[2 * r + 1][h] += o1;
+            acc[2 * r][0] += o0;
+            acc[2 * r + 1][0] += o1;
             if constexpr (r == 0) asm volatile("s_barrier" ::: "memory");  // round-1 writes after round-0 reads
         });
         f32x4 key[M];
 #pragma unroll
-        for (int m = 0; m < M; ++m) key[m] = acc[m][h];
+        for (int m = 0; m < M; ++m) key[m] = acc[m][0];
         if (METRIC == L2) {
             // + |y|^2 of this lane's rows (16 m + rl0 .. +3) from the tile's aux slot
             const uint32_t na = lds_base + V5_AUX_OFF + (uint32_t)(t & 3) * V5_AUX_B + (uint32_t)(rl0 * 4);

@@ -134,6 +134,34 @@ class VectorizationPipeline:
             out[i:i + batch_size] = self._forward_cls(enc)
         return out
 
+    @torch.no_grad()
+    def encode_lengths(self, input_ids: torch.Tensor, lengths, batch_size: int = 256) -> torch.Tensor:
+        """Ragged pre-tokenised path (bench config c): row i of ``input_ids``
+        [n, Lmax] holds ``lengths[i]`` valid tokens.  Rows are sorted by
+        length and every batch is cut to its own longest row (the reference
+        pads per batch, vectorization.py:29-35, but in input order).  Returns
+        [n, hidden] float32 on ``self.device`` in input order.  ``lengths``
+        is read on the host, so the loop never waits on the device."""
+        n = input_ids.shape[0]
+        out = torch.empty((n, self.model.config.hidden_size), dtype=torch.float32, device=self.device)
+        if n == 0:
+            return out
+        lens = torch.as_tensor(lengths, dtype=torch.long).cpu()
+        assert lens.shape[0] == n and int(lens.min()) >= 1 and int(lens.max()) <= input_ids.shape[1], "bad lengths"
+        order = torch.argsort(lens, stable=True)
+        lens_sorted = lens[order]
+        ids = input_ids.to(self.device, non_blocking=True)
+        lens_dev = lens.to(self.device, non_blocking=True)
+        pos = torch.arange(input_ids.shape[1], device=self.device)
+        for i in range(0, n, batch_size):
+            idx = order[i:i + batch_size].to(self.device, non_blocking=True)
+            L = int(lens_sorted[min(i + batch_size, n) - 1])
+            b_ids = ids[idx, :L]
+            mask = (pos[None, :L] < lens_dev[idx][:, None]).to(torch.long)
+            out[idx] = self._forward_cls({"input_ids": b_ids, "attention_mask": mask,
+                                          "token_type_ids": torch.zeros_like(b_ids)})
+        return out
+
     def generate_embeddings(self, texts: List[str], batch_size: int = 32) -> np.ndarray:
         """vectorization.py:18-47: np.ndarray[n, hidden] float32 (np.array([])
         for no texts)."""

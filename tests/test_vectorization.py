@@ -50,3 +50,19 @@ def test_gpu_encoder_matches_cpu_and_hands_off(cpu_pipe):
     ix.add(dev)
     D, I = ix.search(dev, 2)
     assert (I[:, 0].cpu().numpy() == np.arange(len(TEXTS))).all()
+
+
+def test_encode_lengths_matches_unpadded_rows(cpu_pipe):
+    """Length-bucketed ragged batches give each row's own unpadded CLS vector,
+    in input order (padding is masked out of attention)."""
+    g = torch.Generator().manual_seed(7)
+    lens = [5, 40, 12, 3, 33, 17, 9, 26]
+    ids = torch.zeros((len(lens), 48), dtype=torch.long)
+    for i, L in enumerate(lens):
+        ids[i, :L] = torch.randint(1000, 30522, (L,), generator=g)
+        ids[i, 0], ids[i, L - 1] = 101, 102
+    got = cpu_pipe.encode_lengths(ids, lens, batch_size=3).numpy()
+    for i, L in enumerate(lens):
+        one = cpu_pipe.encode_token_batches(ids[i:i + 1, :L], torch.ones((1, L), dtype=torch.long)).numpy()
+        np.testing.assert_allclose(got[i], one[0], rtol=1e-4, atol=1e-4)
+    assert cpu_pipe.encode_lengths(ids[:0], [], batch_size=3).shape == (0, 384)

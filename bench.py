@@ -131,11 +131,18 @@ def cpu_baseline_and_recall(args, n_total, d, k, D, I, nthreads):
     C.knn_blas(xqs, xb, k, nthreads, lib=lib)
     t = time.time() - t0
     qps = nq_s / (t * (n_total / rows))
+    # the reference pins OMP/BLAS to one thread: same port at 1 thread
+    nq_1 = max(16, min(nq_s, int(nq_s * 0.5 / max(nthreads, 1))))
+    t0 = time.time()
+    C.knn_blas(xqs[:nq_1], xb, k, 1, lib=lib)
+    t1 = time.time() - t0
     res["cpu_baseline"] = {
         "value": qps, "unit": "queries/s", "cores": nthreads, "kind": "port",
         "sample": (f"{nq_s} queries x first {rows} rows (fp32) of the same corpus in {t:.2f}s, "
                    f"extrapolated linearly to {n_total} rows; C/OpenMP restatement of faiss "
                    f"IndexFlatL2 BLAS path (oracle/flat_l2.c, {march}); faiss-cpu is not installed"),
+        "value_1thread": nq_1 / (t1 * (n_total / rows)),
+        "sample_1thread": f"{nq_1} queries, same slice, 1 thread, {t1:.2f}s",
     }
     return res
 

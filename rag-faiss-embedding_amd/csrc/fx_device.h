@@ -122,8 +122,16 @@ __device__ __forceinline__ void glds16(const void* gsrc, char* lds_uniform) {
 // in that XCD's L2) and all groups walk the corpus splits in the same order
 // (corpus rows are fetched from HBM about once and re-read from L2/MALL).
 // Placement only changes speed, never results.
+// Alternative (xcd_split > 0, FX_SCAN_MAP=1): XCD x owns a 1/8 slice of the
+// corpus for ALL query tiles and walks it query-tile-major, so the ~32 blocks
+// resident on one XCD stream the SAME split side by side (one fetch per round,
+// L2 hits for the others): corpus traffic ~ n_qtiles/32 x corpus.
 __device__ __forceinline__ void map_block(int b, const ScanParams& p, int& qtile, int& split) {
-    if (p.qt_per_xcd > 0) {
+    if (p.xcd_split > 0) {
+        const int xcd = b & 7, j = b >> 3;
+        qtile = j % p.n_qtiles;
+        split = xcd * p.xcd_split + j / p.n_qtiles;
+    } else if (p.qt_per_xcd > 0) {
         int xcd = b & 7, j = b >> 3;
         qtile = xcd + 8 * (j % p.qt_per_xcd);
         split = j / p.qt_per_xcd;

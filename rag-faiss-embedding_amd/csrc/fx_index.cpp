@@ -147,6 +147,33 @@ hipError_t grow(FxIndex* h, int64_t need_rows) {
 void plan_scan(const FxIndex* h, int64_t nq, ScanParams& p) {
     p.n_qtiles = (int)((nq + TILE_Q - 1) / TILE_Q);
     p.n_ctiles = (int)((h->ntotal + TILE_R - 1) / TILE_R);
+    p.xcd_split = 0;
+    const char* map_env = getenv("FX_SCAN_MAP");
+    if (map_env && atoi(map_env) == 1 && p.n_ctiles >= 8 * 4) {
+        // Corpus-partitioned placement (map_block): splits per XCD such that
+        // (a) each XCD runs >= 4 rounds of its 32 resident blocks, (b) a split
+        // is <= ~512 tiles, so the blocks streaming it side by side drift by
+        // less than the XCD's L2, (c) the last round is as full as possible,
+        // (d) every split keeps >= 4 tiles.  FX_SCAN_SPX overrides.
+        const int s_max = std::max(1, p.n_ctiles / 32);
+        int spx = getenv("FX_SCAN_SPX") ? atoi(getenv("FX_SCAN_SPX")) : 0;
+        if (spx <= 0) {
+            const int s_lo = std::min(s_max, std::max((128 + p.n_qtiles - 1) / p.n_qtiles,
+                                                      (p.n_ctiles + 8 * 512 - 1) / (8 * 512)));
+            spx = s_lo;
+            double best_eff = 0.0;
+            for (int s = s_lo; s <= std::min(s_max, 2 * s_lo); ++s) {
+                const double live = (double)p.n_qtiles * s;
+                const double eff = live / (std::ceil(live / 32.0) * 32.0);
+                if (eff > best_eff + 1e-9) { best_eff = eff; spx = s; }
+                if (eff > 0.985) break;
+            }
+        }
+        p.xcd_split = std::min(spx, s_max);
+        p.splits = 8 * p.xcd_split;
+        p.qt_per_xcd = 0;
+        return;
+    }
     p.qt_per_xcd = p.n_qtiles >= 8 ? (p.n_qtiles + 7) / 8 : 0;
     const int eff_q = p.qt_per_xcd > 0 ? 8 * p.qt_per_xcd : p.n_qtiles;
     // One resident workgroup per CU (150 KiB LDS): pick the split count whose

@@ -50,6 +50,9 @@ struct ScanParams {
     unsigned long long* trace;  // diagnostics only (FX_SCAN_TRACE): per block
                                 // {xcc | hw_id << 8 | qtile << 32, split, t_start, t_end}
     unsigned* dbgbuf;           // diagnostics only (FX_SCAN_DBG & 32): operand self-check
+    int xcd_split;              // > 0: corpus-partitioned placement (FX_SCAN_MAP=1): XCD x owns
+                                // splits [x*xcd_split, (x+1)*xcd_split) of every query tile;
+                                // then splits == 8*xcd_split and qt_per_xcd == 0
 };
 
 struct RefineParams {

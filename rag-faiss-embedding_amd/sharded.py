@@ -74,19 +74,24 @@ class ShardedIndexFlatL2:
             self.local.add(x[a - row0:b - row0])
 
     def search(self, xq, k: int):
-        """Global top-k: local scan -> all_gather of (D, I) -> merge."""
+        """Global top-k: local scan -> ONE all_gather of the packed (D, I)
+        lists (nq*k*12 B per rank) -> merge."""
         D, I = self.local.search(xq, k)
         if self.world == 1:
             return D, I
         is_np = isinstance(D, np.ndarray)
         Dt = torch.from_numpy(D) if is_np else D
         It = torch.from_numpy(I) if is_np else I
-        Dl = [torch.empty_like(Dt) for _ in range(self.world)]
-        Il = [torch.empty_like(It) for _ in range(self.world)]
-        dist.all_gather(Dl, Dt.contiguous(), group=self.group)
-        dist.all_gather(Il, It.contiguous(), group=self.group)
-        Dg = torch.stack(Dl)
-        Ig = torch.stack(Il)
+        nq = Dt.shape[0]
+        # pack each (D f32, I i64) entry as 3 int32 words: one collective per batch
+        mine = torch.empty((nq, k, 3), dtype=torch.int32, device=Dt.device)
+        mine[:, :, 0] = Dt.contiguous().view(torch.int32)
+        mine[:, :, 1:] = It.contiguous().view(torch.int32).view(nq, k, 2)
+        allg = torch.empty((self.world * nq, k, 3), dtype=torch.int32, device=Dt.device)
+        dist.all_gather_into_tensor(allg, mine, group=self.group)
+        allg = allg.view(self.world, nq, k, 3)
+        Dg = allg[..., 0].contiguous().view(torch.float32)
+        Ig = allg[..., 1:].contiguous().view(torch.int64).view(self.world, nq, k)
         Dm, Im = self._merge(Dg, Ig, k)
         if is_np:
             return np.asarray(Dm), np.asarray(Im)

@@ -236,16 +236,21 @@ def main():
     alg_bytes = n_local * d * esize + nq * d * esize + nq * k * 12
     t_scan = scan_avg_ms / 1e3
     mfma_tf = flops / t_scan / 1e12
-    ridge = MFMA_PEAK[dtype] * 1e12 / (HBM_PEAK_GBS * 1e9)
+    peak = MFMA_PEAK[dtype]
+    split = dtype == "float32" and os.environ.get("FX_F32_SPLIT") == "1"
+    if split:  # fp32 index scanned as 3 bf16 products per term (fx_scan.hip F32S)
+        peak = MFMA_PEAK["bfloat16"] / 3.0
+    ridge = peak * 1e12 / (HBM_PEAK_GBS * 1e9)
     if flops / alg_bytes >= ridge:
-        roof = {"bound": "mfma", "achieved": round(mfma_tf, 2), "peak": MFMA_PEAK[dtype], "unit": "TFLOP/s",
-                "frac": round(mfma_tf / MFMA_PEAK[dtype], 4)}
+        roof = {"bound": "mfma", "achieved": round(mfma_tf, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
+                "frac": round(mfma_tf / peak, 4)}
     else:
         gbs = alg_bytes / t_scan / 1e9
         roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(gbs / HBM_PEAK_GBS, 4)}
     roof["traffic"] = read_pmc_traffic(args.config, n_local, nq)
-    roof["kernel"] = "k_scan_v4 (fused MFMA distance GEMM + top-k select)"
+    roof["kernel"] = ("k_scan_v5" if os.environ.get("FX_SCAN_V5") == "1" and not split else "k_scan_v4") + \
+        (" F32S (fp32 as 3 bf16 MFMA products)" if split else "") + " (fused MFMA distance GEMM + top-k select)"
     roof["kernel_ms_avg"] = round(scan_avg_ms, 4)
     roof["launches"] = launches
     roof["merge_refine_ms_avg"] = round(merge_ms / max(launches, 1), 4)

@@ -239,6 +239,8 @@ template <> struct AsmMmaV<F16> {
         }
     }
 };
+// F32S (split fp32) runs on the bf16 pipe; the scan issues the extra products
+template <> struct AsmMmaV<F32S> : AsmMmaV<BF16> {};
 // f32: a 64-B k-chunk is 4 k-steps of 16x16x4; the two columns' dependent
 // chains are interleaved (40-cycle dependent latency vs 32-cycle issue)
 template <> struct AsmMmaV<F32> {

@@ -62,10 +62,10 @@ struct DevBuf {
     size_t bytes = 0;
     hipError_t ensure(size_t want) {
         if (want <= bytes) return hipSuccess;
+        const size_t grow = std::max(want, bytes + bytes / 2);
         if (p) (void)hipFree(p);
         p = nullptr;
         bytes = 0;
-        size_t grow = std::max(want, bytes + bytes / 2);
         hipError_t e = hipMalloc(&p, grow);
         if (e == hipSuccess) bytes = grow;
         return e;
@@ -93,6 +93,9 @@ struct FxIndex {
     hipStream_t user_stream = nullptr;
     // search workspace
     DevBuf qin, qf32, qop, qeps, cand_d, cand_i, dws, iws, flag, fbc_d, fbc_i, stage, gtau, trace, dbgbuf;
+    // F32S scan image of an fp32 index (FX_F32_SPLIT=1): rows [0, split_rows) are current
+    DevBuf split;
+    int64_t split_rows = 0;
     int64_t last_fallbacks = 0;
     // profiling
     bool profile = false;
@@ -209,12 +212,30 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
     HIP_TRY(h->qop.ensure((size_t)nq_pad * h->row_bytes));
     void* qop = h->qop.p;
     HIP_TRY(h->qeps.ensure((size_t)nq * 4));
-    HIP_TRY(launch_prep_queries(qdev, q_dtype, nq, nq_pad, h->d, h->kdim, h->dtype, h->metric, (float*)h->qf32.p,
+    // FX_F32_SPLIT=1: scan an fp32 index through its split-bf16 image (F32S:
+    // 3 bf16 products per term on the bf16 MFMA pipe instead of fp32 MFMA);
+    // the refine and the certification still use the fp32 rows
+    const int rb64 = h->row_bytes / 64;
+    const char* split_env = getenv("FX_F32_SPLIT");
+    const bool split = split_env && atoi(split_env) == 1 && h->dtype == F32 && h->row_bytes % 64 == 0 &&
+                       (rb64 == 8 || rb64 == 12 || rb64 == 16 || rb64 == 24);
+    const int scan_dt = split ? (int)F32S : h->dtype;
+    if (split) {
+        const void* old = h->split.p;
+        HIP_TRY(h->split.ensure((size_t)h->cap_rows * h->row_bytes));
+        if (h->split.p != old || h->split_rows > h->ntotal) {  // fresh buffer: finite (zero) padding rows
+            HIP_TRY(hipMemsetAsync(h->split.p, 0, h->split.bytes, s));
+            h->split_rows = 0;
+        }
+        HIP_TRY(launch_split_rows((const float*)h->codes, h->kdim, h->split_rows, h->ntotal, h->split.p, s));
+        h->split_rows = h->ntotal;
+    }
+    HIP_TRY(launch_prep_queries(qdev, q_dtype, nq, nq_pad, h->d, h->kdim, scan_dt, h->metric, (float*)h->qf32.p,
                                 qop, (float*)h->qeps.p, sqrt((double)h->max_sq), s));
 
     ScanParams sp;
     plan_scan(h, nq, sp);
-    sp.codes = h->codes;
+    sp.codes = split ? (const char*)h->split.p : h->codes;
     sp.norms = h->norms;
     sp.ntotal = h->ntotal;
     sp.row_bytes = h->row_bytes;
@@ -253,7 +274,7 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
         HIP_TRY(hipEventCreate(&e2));
         HIP_TRY(hipEventRecord(e0, s));
     }
-    HIP_TRY(launch_scan(h->dtype, h->metric, sp, s));
+    HIP_TRY(launch_scan(scan_dt, h->metric, sp, s));
     if (h->profile) HIP_TRY(hipEventRecord(e1, s));
 
     float* Dd = D;
@@ -550,6 +571,7 @@ int fx_index_reset(FxIndex* h) {
     }
     h->max_sq = 0.0f;
     h->ntotal = 0;
+    h->split_rows = 0;
     return FX_OK;
 }
 

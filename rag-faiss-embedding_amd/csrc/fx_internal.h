@@ -26,7 +26,12 @@ constexpr int LDS_TAU_OFF = LDS_CNT_OFF + TILE_Q * 4;        // tau   [TILE_Q] f
 constexpr int LDS_FLAG_OFF = LDS_TAU_OFF + TILE_Q * 4;       // overflow flag (16 B)
 constexpr int LDS_SCAN_BYTES = LDS_FLAG_OFF + 16;
 
-enum Dtype { F32 = 0, BF16 = 1, F16 = 2 };
+enum Dtype { F32 = 0, BF16 = 1, F16 = 2,
+             // scan-only operand format of an fp32 index (FX_F32_SPLIT=1): every
+             // value v as bf16 hi = rn(v) and lo = rn(v - hi), rows laid out
+             // [hi plane | lo plane] in the fp32 row's bytes; the scan sums
+             // hi*hi + hi*lo + lo*hi with bf16 MFMAs (never a storage dtype)
+             F32S = 3 };
 enum Metric { IP = 0, L2 = 1 };
 
 inline int dtype_size(int dt) { return dt == F32 ? 4 : 2; }
@@ -92,6 +97,8 @@ hipError_t launch_exact_fallback(int st_dt, int metric, const char* codes, int r
                                  float* D, int64_t* I, hipStream_t s);
 hipError_t launch_merge_shards(int metric, int nshards, int64_t nq, int k, const float* D_in,
                                const int64_t* I_in, float* D_out, int64_t* I_out, hipStream_t s);
+// fp32 code rows [r0, r1) -> their F32S scan image (same row stride)
+hipError_t launch_split_rows(const float* codes, int kdim, int64_t r0, int64_t r1, void* split, hipStream_t s);
 hipError_t launch_synth(void* out, int64_t row0, int64_t n, int d, int dtype, uint64_t seed,
                         hipStream_t s);
 hipError_t launch_to_f32(const void* codes, int st_dt, int row_bytes, int64_t n, int d, float* out,

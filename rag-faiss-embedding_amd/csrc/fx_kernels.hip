@@ -67,6 +67,28 @@ __global__ __launch_bounds__(256) void k_convert_rows(const void* __restrict__ x
     }
 }
 
+// fp32 rows -> F32S scan image: row r = [rn_bf16(v) for v in row | rn_bf16(v - hi)]
+// in the same row_bytes (kdim fp32 = 2 planes of kdim bf16); 4 values per thread
+__global__ __launch_bounds__(256) void k_split_rows(const float* __restrict__ codes, int kdim, int64_t r0,
+                                                    int64_t r1, uint16_t* __restrict__ split) {
+    const int64_t n4 = (r1 - r0) * (int64_t)(kdim / 4);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t row = r0 + i / (kdim / 4);
+        const int c = (int)(i % (kdim / 4)) * 4;
+        const float4 v = *(const float4*)(codes + row * kdim + c);
+        const float vv[4] = {v.x, v.y, v.z, v.w};
+        uint16_t hi[4], lo[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            hi[j] = f2bf(vv[j]);
+            lo[j] = f2bf(vv[j] - bf2f(hi[j]));
+        }
+        uint16_t* out = split + row * (int64_t)(2 * kdim);
+        *(uint2*)(out + c) = make_uint2(hi[0] | ((uint32_t)hi[1] << 16), hi[2] | ((uint32_t)hi[3] << 16));
+        *(uint2*)(out + kdim + c) = make_uint2(lo[0] | ((uint32_t)lo[1] << 16), lo[2] | ((uint32_t)lo[3] << 16));
+    }
+}
+
 // ---------------------------------------------------------------------------
 // search(): query preparation
 // ---------------------------------------------------------------------------
@@ -83,7 +105,15 @@ __global__ __launch_bounds__(256) void k_prep_queries(const void* __restrict__ q
     for (int c = lane; c < kdim; c += 64) {
         float v = (live && c < d) ? load_elem(q, r * d + c, q_dt) : 0.0f;
         qf32[r * (int64_t)kdim + c] = v;
-        {
+        if (st_dt == F32S) {
+            // split scan operand [hi plane | lo plane] of the pre-scaled query
+            // (x' - hi is exact in fp32: hi is within 2^-8 |x'| of x')
+            const float xs = v * (metric == L2 ? -2.0f : -1.0f);
+            const uint16_t hi = f2bf(xs);
+            uint16_t* row = (uint16_t*)qop + r * (int64_t)(2 * kdim);
+            row[c] = hi;
+            row[kdim + c] = f2bf(xs - bf2f(hi));
+        } else {
             // scan operand: x rounded to the storage dtype, pre-scaled (exactly,
             // by a power of two) so that the MFMA accumulator is the key:
             // L2: acc = -2 x.y (+ |y|^2 from the accumulator init); IP: -x.y
@@ -102,7 +132,11 @@ __global__ __launch_bounds__(256) void k_prep_queries(const void* __restrict__ q
         // (u), and the query's rounding to the storage dtype (delta).
         const double u = 5.9604644775390625e-8;  // 2^-24
         const double xn = sqrt(s), M = max_norm;
-        const double delta = inexact ? (st_dt == BF16 ? 3.90625e-3 : 4.8828125e-4) : 0.0;
+        // F32S: the split scan drops lo*lo and both residuals v - hi - lo;
+        // per product <= 3 * 2^-16 (1 + 2^-7) |x_k||y_k|;
+        // gamma then covers its 3 K products (launch_prep_queries)
+        const double delta = st_dt == F32S ? 4.73e-5
+                                           : (inexact ? (st_dt == BF16 ? 3.90625e-3 : 4.8828125e-4) : 0.0);
         double eps;
         if (metric == L2) eps = (2.0 * gamma + u) * (M * M + 2.0 * xn * M) + 2.0 * delta * xn * M;
         else eps = (gamma + u) * xn * M + delta * xn * M;
@@ -601,10 +635,19 @@ hipError_t launch_convert_rows(const void* x, int x_dt, int64_t n, int d, void* 
     return hipGetLastError();
 }
 
+hipError_t launch_split_rows(const float* codes, int kdim, int64_t r0, int64_t r1, void* split, hipStream_t s) {
+    if (r1 <= r0) return hipSuccess;
+    hipLaunchKernelGGL(k_split_rows, dim3(grid_for((r1 - r0) * (kdim / 4), 256, 65536)), dim3(256), 0, s, codes,
+                       kdim, r0, r1, (uint16_t*)split);
+    return hipGetLastError();
+}
+
 hipError_t launch_prep_queries(const void* q, int q_dt, int64_t nq, int64_t nq_pad, int d, int kdim, int st_dt,
                                int metric, float* qf32, void* qop, float* qeps, double max_norm, hipStream_t s) {
     const double u = 5.9604644775390625e-8;
-    const double gamma = (double)kdim * u / (1.0 - (double)kdim * u);
+    // terms accumulated by the scan's fp32 MFMA chain: K products (3 K for F32S) + srcC
+    const double nt = st_dt == F32S ? 3.0 * kdim + 1.0 : (double)kdim;
+    const double gamma = nt * u / (1.0 - nt * u);
     hipLaunchKernelGGL(k_prep_queries, dim3((unsigned)((nq_pad + 3) / 4)), dim3(256), 0, s, q, q_dt, nq, nq_pad, d,
                        kdim, st_dt, metric, qf32, qop, qeps, max_norm, gamma);
     return hipGetLastError();
@@ -624,6 +667,11 @@ static hipError_t scan_t(const ScanParams& p, hipStream_t s) {
 hipError_t launch_scan(int st_dt, int metric, const ScanParams& p, hipStream_t s) {
     // the MFMA scan (fx_scan.hip) covers every row width it has a register
     // layout for; other widths take the generic kernel above
+    if (st_dt == F32S) {  // the split-fp32 operand exists only for the MFMA scan
+        bool handled = false;
+        hipError_t e = launch_scan_mfma(st_dt, metric, p, s, &handled);
+        return handled ? e : hipErrorInvalidValue;
+    }
     if (!getenv("FX_SCAN_V1")) {
         bool handled = false;
         // FX_SCAN_V5=1: the 8-wave K-split scan (fx_scan5.hip), not yet the default

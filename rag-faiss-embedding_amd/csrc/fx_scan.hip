@@ -202,12 +202,18 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
             else
                 asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(W) : "memory");
             __builtin_amdgcn_sched_barrier(0);
+            // F32S (split fp32): stages j < SPT/2 hold the rows' hi plane and
+            // take two passes (x_hi, then x_lo = query K-steps KH..); the lo
+            // plane's stages take one pass against x_hi
+            constexpr int KH = KSTEPS / 2;
+            constexpr bool HI = DT == F32S && 2 * j < KH;
+            constexpr int kq0 = (DT == F32S && !HI) ? 2 * j - KH : 2 * j;  // query K-step of half 0
             // ---- half 0: X MFMAs; read half 1 (Y) of this stage meanwhile
             static_for<M>([&](auto MM) {
                 constexpr int m = decltype(MM)::value;
                 constexpr int INIT = j == 0 ? (METRIC == L2 ? 1 : 2) : 0;
                 if constexpr (!(ABL & 4))
-                    AsmMmaV<DT>::template mma2<INIT>(acc[m][0], acc[m][1], X[m], b[2 * j][0], b[2 * j][1], yin[m]);
+                    AsmMmaV<DT>::template mma2<INIT>(acc[m][0], acc[m][1], X[m], b[kq0][0], b[kq0][1], yin[m]);
                 // half 1 of this stage: two reads per pair over the first four
                 // pairs, so the mid-stage wait finds them landed
                 if constexpr (m < M / 2) {
@@ -224,6 +230,13 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                 if constexpr (m == 4) piece(std::integral_constant<int, 0>{}, JP{}, NXT{}, c4, tnext);
                 if constexpr (m == 6) piece(std::integral_constant<int, 1>{}, JP{}, NXT{}, c4, tnext);
             });
+            if constexpr (HI) {  // hi * x_lo (>= 14 MFMAs after each accumulator's previous write)
+                static_for<M>([&](auto MM) {
+                    constexpr int m = decltype(MM)::value;
+                    AsmMmaV<DT>::template mma2<0>(acc[m][0], acc[m][1], X[m], b[2 * j + KH][0], b[2 * j + KH][1],
+                                                  yin[m]);
+                });
+            }
             if constexpr (LAST) {
                 // epilogue operands of this tile: the queries' thresholds
                 ds_rd32<0>(tr[0], tau_addr);
@@ -239,7 +252,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
             static_for<M>([&](auto MM) {
                 constexpr int m = decltype(MM)::value;
                 if constexpr (!(ABL & 4))
-                    AsmMmaV<DT>::template mma2<0>(acc[m][0], acc[m][1], Y[m], b[2 * j + 1][0], b[2 * j + 1][1], yin[m]);
+                    AsmMmaV<DT>::template mma2<0>(acc[m][0], acc[m][1], Y[m], b[kq0 + 1][0], b[kq0 + 1][1], yin[m]);
                 // half 0 of stage g+1: two reads per pair over the first four
                 // pairs (X[2m+1]'s last reader is >= 8 MFMAs back)
                 if constexpr (m < M / 2) {
@@ -250,6 +263,13 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                 if constexpr (m == 5) piece(std::integral_constant<int, 3>{}, JP{}, NXT{}, c4, tnext);
                 if constexpr (m == 6 && jp == 0) piece(std::integral_constant<int, 4>{}, JP{}, NXT{}, c4, tnext);
             });
+            if constexpr (HI) {
+                static_for<M>([&](auto MM) {
+                    constexpr int m = decltype(MM)::value;
+                    AsmMmaV<DT>::template mma2<0>(acc[m][0], acc[m][1], Y[m], b[2 * j + 1 + KH][0],
+                                                  b[2 * j + 1 + KH][1], yin[m]);
+                });
+            }
             __builtin_amdgcn_sched_barrier(0);
             rd_addr = rd_next;
             c = (int)c1;
@@ -394,6 +414,7 @@ hipError_t launch_scan_mfma(int st_dt, int metric, const ScanParams& p, hipStrea
         *handled = false;
         return hipSuccess;
     }
+    if (st_dt == F32S) return metric == L2 ? scan_rows<F32S, L2>(p, s, handled) : scan_rows<F32S, IP>(p, s, handled);
     if (metric == L2) {
         if (st_dt == F32) return scan_rows<F32, L2>(p, s, handled);
         if (st_dt == BF16) return scan_rows<BF16, L2>(p, s, handled);

@@ -1,0 +1,92 @@
+"""Split-fp32 scan (FX_F32_SPLIT=1): an fp32 index scanned through its
+[hi | lo] bf16 image with 3 bf16 MFMA products per term (fx_scan.hip, F32S).
+
+The scan key changes, the contract does not: results must equal the oracle's
+(ids bit-exact, distances within RTOL) because the refine recomputes the
+candidates' distances from the fp32 rows and certifies them against the
+scan's error bound, which for F32S adds the dropped lo*lo and residual terms:
+    |key - exact| <= (2 gamma_{3K+1} + u)(|y|^2 + 2|x||y|) + 2 * 4.73e-5 |x||y|   (L2)
+    |key - exact| <= (gamma_{3K+1} + u)|x||y| + 4.73e-5 |x||y|                    (IP)
+
+Not yet run on hardware: skipped unless FX_TEST_EXPERIMENTAL=1.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import cpu as C
+from oracle import flat_l2 as F
+from tests.test_gpu_parity import assert_parity
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(os.environ.get("FX_TEST_EXPERIMENTAL") != "1",
+                                 reason="split-fp32 scan not yet validated on MI355X (FX_TEST_EXPERIMENTAL=1)")]
+
+
+@pytest.fixture(scope="module")
+def fx():
+    from rag_faiss_embedding_amd import _lib, faiss
+    if _lib.device_count() == 0:
+        pytest.fail("no GPU visible: -m gpu tests must run on the MI355X box")
+    return faiss
+
+
+@pytest.mark.parametrize("d", [128, 192, 256, 384])
+@pytest.mark.parametrize("metric", ["L2", "IP"])
+def test_split_scan_keys(fx, tmp_path, monkeypatch, d, metric):
+    monkeypatch.setenv("FX_F32_SPLIT", "1")
+    monkeypatch.setenv("FX_SCAN_DBG", "32")
+    path = tmp_path / "keys.bin"
+    monkeypatch.setenv("FX_SCAN_KEYS", str(path))
+    rng = np.random.default_rng(100 + d)
+    n, nq = 1500 + d, 150
+    xb = rng.standard_normal((n, d)).astype(np.float32)
+    xq = rng.standard_normal((nq, d)).astype(np.float32)
+    ix = (fx.IndexFlatL2 if metric == "L2" else fx.IndexFlatIP)(d)
+    ix.add(xb)
+    ix.search(xq, 10)
+    ld = (n + 127) // 128 * 128
+    kv = np.fromfile(path, dtype=np.float32).reshape(-1, ld)[:nq, :n].astype(np.float64)
+    y = xb.astype(np.float64)
+    x = xq.astype(np.float64)
+    dot = x @ y.T
+    ny = (y ** 2).sum(1)[None, :]
+    nx = np.sqrt((x ** 2).sum(1))[:, None]
+    u = 2.0 ** -24
+    K = 3 * d + 1                            # kdim == d for these widths
+    g = K * u / (1 - K * u)
+    if metric == "L2":
+        ref = ny - 2 * dot
+        bound = (2 * g + u) * (ny + 2 * nx * np.sqrt(ny)) + 2 * 4.73e-5 * nx * np.sqrt(ny)
+    else:
+        ref = -dot
+        bound = (g + u) * nx * np.sqrt(ny) + 4.73e-5 * nx * np.sqrt(ny)
+    err = np.abs(kv - ref)
+    assert np.isfinite(kv).all()
+    assert (err <= bound + 1e-30).all(), f"max err/bound {np.max(err / bound):.3g}"
+
+
+@pytest.mark.parametrize("d", [100, 128, 192, 256, 384])
+@pytest.mark.parametrize("metric", ["L2", "IP"])
+def test_split_search_parity(fx, monkeypatch, d, metric):
+    monkeypatch.setenv("FX_F32_SPLIT", "1")
+    rng = np.random.default_rng(7 * d + (metric == "IP"))
+    n, nq = 5000, 300
+    xb = rng.standard_normal((n, d)).astype(np.float32)
+    xb[4000] = xb[17]                       # an exact duplicate: tie -> smaller id
+    xq = rng.standard_normal((nq, d)).astype(np.float32)
+    xq[0] = xb[17]
+    ix = (fx.IndexFlatL2 if metric == "L2" else fx.IndexFlatIP)(d)
+    ix.add(xb[:3000])
+    ix.search(xq[:5], 10)                   # builds the split image of the first 3000 rows
+    ix.add(xb[3000:])                       # ... which the next search extends
+    D, I = ix.search(xq, 10)
+    Dr, Ir = C.knn_exact(xq, xb, 10) if metric == "L2" else F.knn_inner_product(xq, xb, 10)
+    assert_parity(D, I, Dr, Ir)
+    assert ix.last_fallbacks() <= nq // 10
+    ix.reset()
+    ix.add(xb[:700])
+    D, I = ix.search(xq[:50], 5)
+    Dr, Ir = C.knn_exact(xq[:50], xb[:700], 5) if metric == "L2" else F.knn_inner_product(xq[:50], xb[:700], 5)
+    assert_parity(D, I, Dr, Ir)

@@ -1,10 +1,16 @@
 #!/bin/bash
-# First GPU session for the 8-wave scan (k_scan_v5, FX_SCAN_V5=1): key-matrix
-# and parity tests with v5 selected, then config (d) with v4 and v5 back to
-# back, each also with the corpus-partitioned placement.  Stops at the first failure (a fault ends the call: no retries).
+# First GPU session for the opt-in scan variants written without hardware:
+#   * the 8-wave K-split scan (k_scan_v5, FX_SCAN_V5=1),
+#   * the corpus-partitioned XCD placement (FX_SCAN_MAP=1),
+#   * the split-fp32 scan of fp32 indexes (FX_F32_SPLIT=1).
+# Key-matrix and parity tests first, then config (d) / (b) benches back to
+# back.  Stops at the first failure (a fault ends the call: no retries).
 set -euo pipefail
-out=gpurun_out/${1:-v5}
+out=gpurun_out/${1:-exp}
 mkdir -p "$out"
+FX_TEST_EXPERIMENTAL=1 timeout -k 10 300 python -u -m pytest tests/test_f32_split.py -x -v --timeout 120 --timeout-method thread > "$out/split.log" 2>&1
+timeout -k 10 240 python -u bench.py --config b --no-cpu > "$out/bench_b.json" 2> "$out/bench_b.err"
+FX_F32_SPLIT=1 timeout -k 10 240 python -u bench.py --config b --no-cpu > "$out/bench_b_split.json" 2> "$out/bench_b_split.err"
 FX_SCAN_V5=1 timeout -k 10 300 python -u -m pytest tests/test_scan_keys.py -x -v --timeout 120 --timeout-method thread > "$out/keys_v5.log" 2>&1
 FX_SCAN_V5=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 120 --timeout-method thread > "$out/parity_v5.log" 2>&1
 timeout -k 10 300 python -u bench.py --no-cpu > "$out/bench_d_v4.json" 2> "$out/bench_d_v4.err"

@@ -13,6 +13,7 @@ usage: tools/summarize_profile.py <prof_dir> <tag> <round> <rows_per_gpu> <nq>
 """
 import csv
 import json
+import os
 import shutil
 import statistics
 import sys
@@ -20,7 +21,7 @@ from collections import defaultdict
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-SCAN = "k_scan_v4"
+SCAN = os.environ.get("FX_PROFILE_KERNEL", "k_scan_v")  # k_scan_v4 / k_scan_v5
 
 
 def counters(path):

@@ -151,6 +151,18 @@ void plan_scan(const FxIndex* h, int64_t nq, ScanParams& p) {
     p.n_qtiles = (int)((nq + TILE_Q - 1) / TILE_Q);
     p.n_ctiles = (int)((h->ntotal + TILE_R - 1) / TILE_R);
     p.xcd_split = 0;
+    p.q32_tiles = 0;
+    const int rb64 = h->row_bytes / 64;
+    const char* q32_env = getenv("FX_SCAN_Q32");
+    if (q32_env && atoi(q32_env) == 1 && nq <= 32 && h->row_bytes % 64 == 0 &&
+        (rb64 == 8 || rb64 == 12 || rb64 == 16 || rb64 == 24)) {
+        // small batch (k_scan_q32): one 32-query tile; one round of one
+        // workgroup per CU, each split >= 4 tiles; every corpus byte read once
+        p.q32_tiles = (int)((nq + 31) / 32);
+        p.qt_per_xcd = 0;
+        p.splits = std::max(1, std::min(p.n_ctiles / 4, 256 / p.q32_tiles));
+        return;
+    }
     const char* map_env = getenv("FX_SCAN_MAP");
     if (map_env && atoi(map_env) == 1 && p.n_ctiles >= 8 * 4) {
         // Corpus-partitioned placement (map_block): splits per XCD such that
@@ -245,14 +257,17 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
     HIP_TRY(h->gtau.ensure((size_t)sp.n_qtiles * TILE_Q * 4));
     sp.gtau = (unsigned*)h->gtau.p;
     HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)sp.gtau, 0xff800000u, (size_t)sp.n_qtiles * TILE_Q, s));  // ord(+inf)
-    const size_t ncand = (size_t)sp.n_qtiles * sp.splits * TILE_Q * KP;
+    // candidate lists per (query, split): k_scan_q32's 4 waves each emit one
+    const int cand_splits = sp.q32_tiles > 0 ? 4 * sp.splits : sp.splits;
+    const size_t ncand = (size_t)sp.n_qtiles * cand_splits * TILE_Q * KP;
     HIP_TRY(h->cand_d.ensure(ncand * 4));
     HIP_TRY(h->cand_i.ensure(ncand * 4));
     sp.cand_d = (float*)h->cand_d.p;
     sp.cand_i = (int*)h->cand_i.p;
     // diagnostics: per-block placement/timing of the scan -> binary file
     const char* trace_path = getenv("FX_SCAN_TRACE");
-    const size_t grid = (size_t)(sp.qt_per_xcd > 0 ? 8 * sp.qt_per_xcd : sp.n_qtiles) * sp.splits;
+    const size_t grid = (size_t)(sp.q32_tiles > 0 ? sp.q32_tiles : sp.qt_per_xcd > 0 ? 8 * sp.qt_per_xcd : sp.n_qtiles) *
+                        sp.splits;
     sp.trace = nullptr;
     sp.dbgbuf = nullptr;
     const size_t nkeys = (size_t)sp.n_qtiles * TILE_Q * sp.n_ctiles * TILE_R;
@@ -292,7 +307,7 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
     RefineParams rp;
     rp.cand_d = sp.cand_d;
     rp.cand_i = sp.cand_i;
-    rp.splits = sp.splits;
+    rp.splits = cand_splits;
     rp.nq = nq;
     rp.k = k;
     rp.codes = h->codes;

@@ -58,6 +58,9 @@ struct ScanParams {
     int xcd_split;              // > 0: corpus-partitioned placement (FX_SCAN_MAP=1): XCD x owns
                                 // splits [x*xcd_split, (x+1)*xcd_split) of every query tile;
                                 // then splits == 8*xcd_split and qt_per_xcd == 0
+    int q32_tiles;              // > 0: small-batch scan k_scan_q32 (FX_SCAN_Q32=1) over this many
+                                // 32-query tiles; its 4 waves emit 4 lists per split (refine
+                                // sees 4*splits)
 };
 
 struct RefineParams {
@@ -90,6 +93,8 @@ hipError_t launch_scan(int st_dt, int metric, const ScanParams& p, hipStream_t s
 hipError_t launch_scan_mfma(int st_dt, int metric, const ScanParams& p, hipStream_t s, bool* handled);
 // fx_scan5.hip: the 8-wave K-split variant (selected by FX_SCAN_V5=1)
 hipError_t launch_scan_mfma5(int st_dt, int metric, const ScanParams& p, hipStream_t s, bool* handled);
+// fx_scan_q32.hip: the small-batch scan (p.q32_tiles > 0)
+hipError_t launch_scan_q32(int st_dt, int metric, const ScanParams& p, hipStream_t s, bool* handled);
 hipError_t launch_refine(int st_dt, int metric, const RefineParams& p, hipStream_t s);
 hipError_t launch_exact_fallback(int st_dt, int metric, const char* codes, int row_bytes, int kdim,
                                  int64_t ntotal, const float* qf32, const int* qlist, int nlist,

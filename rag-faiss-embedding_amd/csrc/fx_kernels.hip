@@ -667,6 +667,11 @@ static hipError_t scan_t(const ScanParams& p, hipStream_t s) {
 hipError_t launch_scan(int st_dt, int metric, const ScanParams& p, hipStream_t s) {
     // the MFMA scan (fx_scan.hip) covers every row width it has a register
     // layout for; other widths take the generic kernel above
+    if (p.q32_tiles > 0) {  // small batch: k_scan_q32 (fx_scan_q32.hip); the host planned for it
+        bool handled = false;
+        hipError_t e = launch_scan_q32(st_dt, metric, p, s, &handled);
+        return handled ? e : hipErrorInvalidValue;
+    }
     if (st_dt == F32S) {  // the split-fp32 operand exists only for the MFMA scan
         bool handled = false;
         hipError_t e = launch_scan_mfma(st_dt, metric, p, s, &handled);

@@ -2,13 +2,19 @@
 # First GPU session for the opt-in scan variants written without hardware:
 #   * the 8-wave K-split scan (k_scan_v5, FX_SCAN_V5=1),
 #   * the corpus-partitioned XCD placement (FX_SCAN_MAP=1),
-#   * the split-fp32 scan of fp32 indexes (FX_F32_SPLIT=1).
+#   * the split-fp32 scan of fp32 indexes (FX_F32_SPLIT=1),
+#   * the small-batch scan k_scan_q32 (FX_SCAN_Q32=1).
 # Key-matrix and parity tests first, then config (d) / (b) benches back to
 # back.  Stops at the first failure (a fault ends the call: no retries).
 set -euo pipefail
 out=gpurun_out/${1:-exp}
 mkdir -p "$out"
 FX_TEST_EXPERIMENTAL=1 timeout -k 10 300 python -u -m pytest tests/test_f32_split.py -x -v --timeout 120 --timeout-method thread > "$out/split.log" 2>&1
+FX_TEST_EXPERIMENTAL=1 timeout -k 10 300 python -u -m pytest tests/test_q32.py -x -v --timeout 120 --timeout-method thread > "$out/q32.log" 2>&1
+for nq in 1 32; do
+  timeout -k 10 240 python -u bench.py --config d --nq $nq --no-cpu --steps 20 >> "$out/nq_d_v4.jsonl" 2>> "$out/nq.err"
+  FX_SCAN_Q32=1 timeout -k 10 240 python -u bench.py --config d --nq $nq --no-cpu --steps 20 >> "$out/nq_d_q32.jsonl" 2>> "$out/nq.err"
+done
 timeout -k 10 240 python -u bench.py --config b --no-cpu > "$out/bench_b.json" 2> "$out/bench_b.err"
 FX_F32_SPLIT=1 timeout -k 10 240 python -u bench.py --config b --no-cpu > "$out/bench_b_split.json" 2> "$out/bench_b_split.err"
 FX_SCAN_V5=1 timeout -k 10 300 python -u -m pytest tests/test_scan_keys.py -x -v --timeout 120 --timeout-method thread > "$out/keys_v5.log" 2>&1

@@ -71,19 +71,20 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_sharded_search_world2_gloo():
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_search_gloo(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(timeout=180)
-    res = sorted(q.get(timeout=5) for _ in range(2))
+    res = sorted(q.get(timeout=5) for _ in range(world))
     assert all(p.exitcode == 0 for p in procs)
     assert all(ok for _, ok, _ in res), res
-    assert res[0][2] == res[1][2]
+    assert all(r[2] == res[0][2] for r in res)
 
 
 def test_shard_bounds_cover_rows():

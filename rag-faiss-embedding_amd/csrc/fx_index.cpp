@@ -257,8 +257,7 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
     HIP_TRY(h->gtau.ensure((size_t)sp.n_qtiles * TILE_Q * 4));
     sp.gtau = (unsigned*)h->gtau.p;
     HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)sp.gtau, 0xff800000u, (size_t)sp.n_qtiles * TILE_Q, s));  // ord(+inf)
-    // candidate lists per (query, split): k_scan_q32's 4 waves each emit one
-    const int cand_splits = sp.q32_tiles > 0 ? 4 * sp.splits : sp.splits;
+    const int cand_splits = sp.splits;  // one candidate list per (query, split)
     const size_t ncand = (size_t)sp.n_qtiles * cand_splits * TILE_Q * KP;
     HIP_TRY(h->cand_d.ensure(ncand * 4));
     HIP_TRY(h->cand_i.ensure(ncand * 4));

@@ -59,8 +59,7 @@ struct ScanParams {
                                 // splits [x*xcd_split, (x+1)*xcd_split) of every query tile;
                                 // then splits == 8*xcd_split and qt_per_xcd == 0
     int q32_tiles;              // > 0: small-batch scan k_scan_q32 (FX_SCAN_Q32=1) over this many
-                                // 32-query tiles; its 4 waves emit 4 lists per split (refine
-                                // sees 4*splits)
+                                // 32-query tiles (one workgroup per tile and split)
 };
 
 struct RefineParams {

@@ -14,9 +14,10 @@
 //   * a stage's 4 fragments are read one stage ahead into a second register
 //     set, hiding the LDS latency behind the current stage's 8 MFMAs and the
 //     wave's 4 DMA issues;
-//   * each wave keeps its own top-KP lists for the 32 queries; they leave as
-//     4 candidate lists per (query, corpus split) -- split index 4 s + w in
-//     the refine's [query tile of 128][split][128][KP] layout.
+//   * each wave keeps its own top-KP lists for the 32 queries; after the scan
+//     the 4 waves' lists are merged in LDS (one barrier) into one list per
+//     (query, corpus split), in the refine's [query tile of 128][split][128][KP]
+//     layout.
 //
 // Not yet measured on hardware: selected only with FX_SCAN_Q32=1.
 #include "fx_scan_common.h"
@@ -294,18 +295,34 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_q32(ScanParams p) {
     }
 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
-    // this wave's sorted top-KP per query -> split 4*split + wave of the
-    // 128-query tile that holds these 32 queries
-    const int splits_eff = 4 * p.splits;
-    const int64_t qt128 = q0 / TILE_Q, qoff = q0 % TILE_Q;
-    const int64_t obase = (qt128 * splits_eff + 4 * split + wave) * TILE_Q + qoff;
+    // each wave: its sorted top-KP per query, in place (missing entries +inf)
     for (int qi = 0; qi < 32; ++qi) {
-        if (q0 + qi >= p.nq) break;
         const int q = sw0 + qi;
         const int cn = min(cnt[q], CAP);
         float d = lane < cn ? lst_d[q * CAP + lane] : FX_INF;
         int i = lane < cn ? lst_i[q * CAP + lane] : INT_MAX;
         sort64(d, i, lane);
+        if (lane < KP) {
+            lst_d[q * CAP + lane] = d;
+            lst_i[q * CAP + lane] = i;
+        }
+    }
+    __syncthreads();
+    // wave w merges queries 8w .. 8w+7 over the 4 waves' lists -> one list
+    // per (query, split) in the refine's [query tile of 128][split][128][KP]
+    const int64_t qt128 = q0 / TILE_Q, qoff = q0 % TILE_Q;
+    const int64_t obase = (qt128 * p.splits + split) * TILE_Q + qoff;
+    for (int qq = 0; qq < 8; ++qq) {
+        const int qi = wave * 8 + qq;
+        if (q0 + qi >= p.nq) break;
+        const int s0 = (lane >> 5) * 32 + qi, s1 = (2 + (lane >> 5)) * 32 + qi;  // slots of waves 0/1, 2/3
+        float d = lst_d[s0 * CAP + (lane & 31)];
+        int i = lst_i[s0 * CAP + (lane & 31)];
+        float d2 = lst_d[s1 * CAP + (lane & 31)];
+        int i2 = lst_i[s1 * CAP + (lane & 31)];
+        sort64(d, i, lane);
+        sort64(d2, i2, lane);
+        merge_into(d, i, d2, i2, lane);
         if (lane < KP) {
             p.cand_d[(obase + qi) * KP + lane] = d;
             p.cand_i[(obase + qi) * KP + lane] = i == INT_MAX ? -1 : i;

@@ -319,6 +319,7 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
     rp.I = Id;
     rp.n_flag = n_flag;
     rp.flag_list = n_flag + 1;
+    rp.prefetch = sp.q32_tiles > 0 ? 4 : 1;
     HIP_TRY(launch_refine(h->dtype, h->metric, rp, s));
     if (h->profile) {
         HIP_TRY(hipEventRecord(e2, s));

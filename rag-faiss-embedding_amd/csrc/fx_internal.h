@@ -78,6 +78,7 @@ struct RefineParams {
     int64_t* I;
     int* n_flag;           // uncertified counter
     int* flag_list;        // [nq] uncertified query ids
+    int prefetch;          // > 1: phase-1 loads issued 4 chunks at a time (small-batch scan)
 };
 
 // launchers (stream-ordered, no host sync) -- fx_kernels.hip

@@ -402,7 +402,23 @@ __device__ __forceinline__ double exact_partial(const float* __restrict__ xq, co
     return acc;
 }
 
-template <int DT, int METRIC>
+// merge one chunk of 64 candidates (one per lane) into the running best-64
+__device__ __forceinline__ void refine_take(float d, int i, float& bd, int& bi, float& td, int& ti, int& nvalid,
+                                            int lane) {
+    nvalid += __popcll(__ballot(i != INT_MAX));
+    const bool pass = i != INT_MAX && key_lt(d, i, td, ti);
+    if (!__any(pass)) return;
+    if (!pass) { d = FX_INF; i = INT_MAX; }
+    sort64(d, i, lane);
+    merge_into(bd, bi, d, i, lane);
+    td = __shfl(bd, KP - 1, 64);
+    ti = __shfl(bi, KP - 1, 64);
+}
+
+// PF = chunks of 64 candidates whose loads are issued together in phase 1
+// (PF = 4 for the small-batch scan's many splits: one wave per query is
+// latency-bound on one dependent load per chunk otherwise)
+template <int DT, int METRIC, int PF = 1>
 __global__ __launch_bounds__(256) void k_refine(RefineParams p) {
     const int lane = threadIdx.x & 63;
     const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -414,24 +430,46 @@ __global__ __launch_bounds__(256) void k_refine(RefineParams p) {
     float bd = FX_INF, td = FX_INF;
     int bi = INT_MAX, ti = INT_MAX;
     int nvalid = 0;
-    for (int base = 0; base < ncand; base += 64) {
-        const int c = base + lane;
-        float d = FX_INF;
-        int i = INT_MAX;
-        if (c < ncand) {
-            const int s = c / KP, j = c - s * KP;
-            const int64_t off = (((int64_t)qtile * p.splits + s) * TILE_Q + qq) * KP + j;
-            const int ii = p.cand_i[off];
-            if (ii >= 0) { d = p.cand_d[off]; i = ii; }
+    if constexpr (PF > 1) {
+        for (int base = 0; base < ncand; base += 64 * PF) {
+            float dv[PF];
+            int iv[PF];
+#pragma unroll
+            for (int u = 0; u < PF; ++u) {
+                const int c = base + u * 64 + lane;
+                dv[u] = FX_INF;
+                iv[u] = INT_MAX;
+                if (c < ncand) {
+                    const int s = c / KP, j = c - s * KP;
+                    const int64_t off = (((int64_t)qtile * p.splits + s) * TILE_Q + qq) * KP + j;
+                    const float dd = p.cand_d[off];  // both loads in flight together
+                    const int ii = p.cand_i[off];
+                    if (ii >= 0) { dv[u] = dd; iv[u] = ii; }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < PF; ++u) refine_take(dv[u], iv[u], bd, bi, td, ti, nvalid, lane);
         }
-        nvalid += __popcll(__ballot(i != INT_MAX));
-        const bool pass = i != INT_MAX && key_lt(d, i, td, ti);
-        if (!__any(pass)) continue;
-        if (!pass) { d = FX_INF; i = INT_MAX; }
-        sort64(d, i, lane);
-        merge_into(bd, bi, d, i, lane);
-        td = __shfl(bd, KP - 1, 64);
-        ti = __shfl(bi, KP - 1, 64);
+    } else {
+        for (int base = 0; base < ncand; base += 64) {
+            const int c = base + lane;
+            float d = FX_INF;
+            int i = INT_MAX;
+            if (c < ncand) {
+                const int s = c / KP, j = c - s * KP;
+                const int64_t off = (((int64_t)qtile * p.splits + s) * TILE_Q + qq) * KP + j;
+                const int ii = p.cand_i[off];
+                if (ii >= 0) { d = p.cand_d[off]; i = ii; }
+            }
+            nvalid += __popcll(__ballot(i != INT_MAX));
+            const bool pass = i != INT_MAX && key_lt(d, i, td, ti);
+            if (!__any(pass)) continue;
+            if (!pass) { d = FX_INF; i = INT_MAX; }
+            sort64(d, i, lane);
+            merge_into(bd, bi, d, i, lane);
+            td = __shfl(bd, KP - 1, 64);
+            ti = __shfl(bi, KP - 1, 64);
+        }
     }
 
     // ---- phase 2: exact fp64 values of the KP selected rows (16 lanes / row)
@@ -696,7 +734,10 @@ hipError_t launch_scan(int st_dt, int metric, const ScanParams& p, hipStream_t s
 
 template <int DT, int METRIC>
 static hipError_t refine_t(const RefineParams& p, hipStream_t s) {
-    hipLaunchKernelGGL((k_refine<DT, METRIC>), dim3((unsigned)((p.nq + 3) / 4)), dim3(256), 0, s, p);
+    if (p.prefetch > 1)
+        hipLaunchKernelGGL((k_refine<DT, METRIC, 4>), dim3((unsigned)((p.nq + 3) / 4)), dim3(256), 0, s, p);
+    else
+        hipLaunchKernelGGL((k_refine<DT, METRIC>), dim3((unsigned)((p.nq + 3) / 4)), dim3(256), 0, s, p);
     return hipGetLastError();
 }
 

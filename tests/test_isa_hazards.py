@@ -1,0 +1,58 @@
+"""Static ISA check of the hand-scheduled LDS-DMA scan kernels (CPU only).
+
+Compiles every scan translation unit to gfx950 assembly and runs
+tools/check_dma_hazards.py over it: no LDS-DMA may read an SGPR base written
+by a VALU instruction less than 5 wait states earlier, and no LDS-DMA may
+directly follow an M0 write.  Both hazards reached the hardware once in this
+repo's history -- the compiler does not insert wait states
+in front of inline asm -- and a register-allocation change can reintroduce
+them without any source edit in the kernel.
+"""
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+CSRC = ROOT / "rag-faiss-embedding_amd" / "csrc"
+HIPCC = "/opt/rocm/bin/hipcc"
+UNITS = ["fx_scan.hip", "fx_scan5.hip", "fx_scan_q32.hip"]
+
+pytestmark = pytest.mark.skipif(not Path(HIPCC).exists(), reason="hipcc not available")
+
+
+@pytest.fixture(scope="module")
+def asm_files(tmp_path_factory):
+    out = tmp_path_factory.mktemp("isa")
+    procs = {}
+    for u in UNITS:
+        s = out / (u + ".s")
+        procs[u] = (s, subprocess.Popen([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only",
+                                         "-S", str(CSRC / u), "-o", str(s)], stdout=subprocess.DEVNULL,
+                                        stderr=subprocess.PIPE))
+    res = {}
+    for u, (s, p) in procs.items():
+        _, err = p.communicate(timeout=600)
+        assert p.returncode == 0, err.decode()[-2000:]
+        res[u] = s
+    yield res
+    shutil.rmtree(out, ignore_errors=True)
+
+
+@pytest.mark.parametrize("unit", UNITS)
+def test_no_dma_hazards(asm_files, unit):
+    r = subprocess.run([sys.executable, str(ROOT / "tools" / "check_dma_hazards.py"), str(asm_files[unit])],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-3000:]
+    assert "0 hazard(s)" in r.stdout
+
+
+def test_checker_flags_known_hazards(tmp_path):
+    s = tmp_path / "bad.s"
+    s.write_text("\tv_readfirstlane_b32 s9, v1\n\ts_nop 1\n\tglobal_load_lds_dwordx4 v2, s[8:9] offset:64\n"
+                 "\ts_mov_b32 m0, s3\n\tglobal_load_lds_dwordx4 v2, s[10:11] offset:64\n")
+    r = subprocess.run([sys.executable, str(ROOT / "tools" / "check_dma_hazards.py"), str(s)],
+                       capture_output=True, text=True)
+    assert r.returncode == 1 and "2 hazard(s)" in r.stdout

@@ -248,7 +248,9 @@ def main():
         gbs = alg_bytes / t_scan / 1e9
         roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(gbs / HBM_PEAK_GBS, 4)}
-    roof["traffic"] = read_pmc_traffic(args.config, n_local, nq)
+    # the committed PMC pass measured the default scan: no traffic figure for an opt-in variant
+    variant = any(os.environ.get(v) == "1" for v in ("FX_SCAN_V5", "FX_SCAN_MAP", "FX_SCAN_Q32", "FX_F32_SPLIT"))
+    roof["traffic"] = None if variant else read_pmc_traffic(args.config, n_local, nq)
     scan_kernel = ("k_scan_q32" if os.environ.get("FX_SCAN_Q32") == "1" and nq <= 32 else
                    "k_scan_v5" if os.environ.get("FX_SCAN_V5") == "1" and not split else "k_scan_v4")
     roof["kernel"] = scan_kernel + \

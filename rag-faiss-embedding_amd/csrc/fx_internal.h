@@ -91,8 +91,8 @@ hipError_t launch_prep_queries(const void* q, int q_dt, int64_t nq, int64_t nq_p
 hipError_t launch_scan(int st_dt, int metric, const ScanParams& p, hipStream_t s);
 // fx_scan.hip: the MFMA scan; *handled = false when it has no kernel for p.row_bytes
 hipError_t launch_scan_mfma(int st_dt, int metric, const ScanParams& p, hipStream_t s, bool* handled);
-// fx_scan5.hip: the 8-wave K-split variant (selected by FX_SCAN_V5=1)
-hipError_t launch_scan_mfma5(int st_dt, int metric, const ScanParams& p, hipStream_t s, bool* handled);
+// fx_scan5.hip: the 8-wave K-split variant (FX_SCAN_V5=1; =2 with the staggered epilogue)
+hipError_t launch_scan_mfma5(int st_dt, int metric, const ScanParams& p, hipStream_t s, bool stag, bool* handled);
 // fx_scan_q32.hip: the small-batch scan (p.q32_tiles > 0)
 hipError_t launch_scan_q32(int st_dt, int metric, const ScanParams& p, hipStream_t s, bool* handled);
 hipError_t launch_refine(int st_dt, int metric, const RefineParams& p, hipStream_t s);

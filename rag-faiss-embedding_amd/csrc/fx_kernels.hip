@@ -718,8 +718,9 @@ hipError_t launch_scan(int st_dt, int metric, const ScanParams& p, hipStream_t s
     if (!getenv("FX_SCAN_V1")) {
         bool handled = false;
         // FX_SCAN_V5=1: the 8-wave K-split scan (fx_scan5.hip), not yet the default
-        static const bool v5 = getenv("FX_SCAN_V5") != nullptr && atoi(getenv("FX_SCAN_V5")) != 0;
-        hipError_t e = v5 ? launch_scan_mfma5(st_dt, metric, p, s, &handled) : launch_scan_mfma(st_dt, metric, p, s, &handled);
+        static const int v5 = getenv("FX_SCAN_V5") != nullptr ? atoi(getenv("FX_SCAN_V5")) : 0;
+        hipError_t e = v5 ? launch_scan_mfma5(st_dt, metric, p, s, v5 == 2, &handled)
+                          : launch_scan_mfma(st_dt, metric, p, s, &handled);
         if (handled) return e;
     }
     if (metric == L2) {

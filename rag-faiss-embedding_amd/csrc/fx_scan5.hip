@@ -33,32 +33,38 @@ constexpr int V5_THREADS = 512;
 constexpr int V5_TR = 64;                          // corpus rows per tile
 constexpr int V5_NS = 5;                           // ring slots
 constexpr int V5_STAGE = V5_TR * 256;              // 16 KiB: 64 rows x (2 halves x 128 B)
-constexpr int V5_CAP = 48;                         // LDS list capacity per query (> KP)
-constexpr int V5_AUX_B = 256 + TILE_Q * 4;         // per tile: 64 norms + 128 thresholds
-constexpr int V5_AUX_OFF = 0;                      // 4 tile slots of aux data
-constexpr int V5_RING_OFF = 4096;                  // >= any DMA instruction offset (dma_piece)
-constexpr int V5_XCH_OFF = V5_RING_OFF + V5_NS * V5_STAGE;
-constexpr int V5_XCH_B = 16384;                    // one exchange round: 8 waves x 2 KiB
-constexpr int V5_LD_OFF = V5_XCH_OFF + V5_XCH_B;
-constexpr int V5_LI_OFF = V5_LD_OFF + TILE_Q * V5_CAP * 4;
-constexpr int V5_CNT_OFF = V5_LI_OFF + TILE_Q * V5_CAP * 4;
-constexpr int V5_TAU_OFF = V5_CNT_OFF + TILE_Q * 4;
-constexpr int V5_LDS_BYTES = V5_TAU_OFF + TILE_Q * 4;
-static_assert(4 * V5_AUX_B <= V5_RING_OFF, "aux slots");
-static_assert(V5_LDS_BYTES <= 160 * 1024, "LDS budget");
+// LDS carve.  STAG = 1 (staggered epilogue) exchanges all four partner blocks
+// in one round (32 KiB) and keeps 40-entry lists to stay within 160 KiB.
+template <int STAG>
+struct V5Lds {
+    static constexpr int CAPV = STAG ? 40 : 48;            // LDS list capacity per query (> KP)
+    static constexpr int AUX_B = 256 + TILE_Q * 4;         // per tile: 64 norms + 128 thresholds
+    static constexpr int AUX_OFF = 0;                      // 4 tile slots of aux data
+    static constexpr int RING_OFF = 4096;                  // >= any DMA instruction offset (dma_piece)
+    static constexpr int XCH_OFF = RING_OFF + V5_NS * V5_STAGE;
+    static constexpr int XCH_B = STAG ? 32768 : 16384;     // exchange: 8 waves x 4 (2) KiB
+    static constexpr int LD_OFF = XCH_OFF + XCH_B;
+    static constexpr int LI_OFF = LD_OFF + TILE_Q * CAPV * 4;
+    static constexpr int CNT_OFF = LI_OFF + TILE_Q * CAPV * 4;
+    static constexpr int TAU_OFF = CNT_OFF + TILE_Q * 4;
+    static constexpr int BYTES = TAU_OFF + TILE_Q * 4;
+    static_assert(4 * AUX_B <= RING_OFF, "aux slots");
+    static_assert(BYTES <= 160 * 1024, "LDS budget");
+};
 
 // Compact the wave's full lists (16 queries from q_first) to their KP best.
+template <int CAPV>
 __device__ __noinline__ void compact16(float* lst_d, int* lst_i, int* cnt, float* tau, unsigned* gt_first,
                                        int q_first, int lane) {
     for (int qi = 0; qi < 16; ++qi) {
         const int q = q_first + qi;
-        if (cnt[q] >= V5_CAP) {
-            float d = lane < V5_CAP ? lst_d[q * V5_CAP + lane] : FX_INF;
-            int i = lane < V5_CAP ? lst_i[q * V5_CAP + lane] : INT_MAX;
+        if (cnt[q] >= CAPV) {
+            float d = lane < CAPV ? lst_d[q * CAPV + lane] : FX_INF;
+            int i = lane < CAPV ? lst_i[q * CAPV + lane] : INT_MAX;
             sort64(d, i, lane);
             if (lane < KP) {
-                lst_d[q * V5_CAP + lane] = d;
-                lst_i[q * V5_CAP + lane] = i;
+                lst_d[q * CAPV + lane] = d;
+                lst_i[q * CAPV + lane] = i;
             }
             if (lane == KP - 1) {
                 tau[q] = d;
@@ -70,7 +76,8 @@ __device__ __noinline__ void compact16(float* lst_d, int* lst_i, int* cnt, float
 }
 
 // push the eligible entries of key group m (4 rows of this lane) into query
-// q's list (capacity V5_CAP); list-full entries -> pend bit 4m+i
+// q's list (capacity CAPV); list-full entries -> pend bit 4m+i
+template <int CAPV>
 __device__ __forceinline__ bool push4(const f32x4& key, int m, unsigned elig, float tn, int q, int row0, int rlim,
                                       float* lst_d, int* lst_i, int* cnt, unsigned& pend) {
     bool ovf = false;
@@ -80,9 +87,9 @@ __device__ __forceinline__ bool push4(const f32x4& key, int m, unsigned elig, fl
         const int rl = row0 + i;
         if (((elig >> i) & 1u) && v <= tn && rl < rlim) {
             const int s = atomicAdd(&cnt[q], 1);
-            if (s < V5_CAP) {
-                lst_d[q * V5_CAP + s] = v;
-                lst_i[q * V5_CAP + s] = rl;
+            if (s < CAPV) {
+                lst_d[q * CAPV + s] = v;
+                lst_i[q * CAPV + s] = rl;
             } else {
                 pend |= 1u << (m * 4 + i);
                 ovf = true;
@@ -105,7 +112,7 @@ __device__ __forceinline__ void ds_wr128(uint32_t addr, const f32x4& v) {
     asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(addr), "v"(v), "i"(OFF) : "memory");
 }
 
-template <int DT, int METRIC, int KSTEPS>
+template <int DT, int METRIC, int KSTEPS, int STAG>
 __global__ __launch_bounds__(V5_THREADS, 1) void k_scan_v5(ScanParams p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     typedef typename AsmMmaV<DT>::A frag_t;
@@ -119,6 +126,8 @@ __global__ __launch_bounds__(V5_THREADS, 1) void k_scan_v5(ScanParams p) {
     constexpr int M = V5_TR / 16;         // 4 row blocks
     constexpr int N = 2;                  // query columns of 16
     constexpr int64_t TB = (int64_t)V5_TR * RB;
+    typedef V5Lds<STAG> L;
+    constexpr int CAPV = L::CAPV;
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -127,15 +136,17 @@ __global__ __launch_bounds__(V5_THREADS, 1) void k_scan_v5(ScanParams p) {
     map_block(blockIdx.x, p, qtile, split);
     if (qtile >= p.n_qtiles) return;
     const int n64 = (int)((p.ntotal + V5_TR - 1) / V5_TR);
-    const int ct0 = (int)((int64_t)split * n64 / p.splits);
-    const int ct1 = (int)((int64_t)(split + 1) * n64 / p.splits);
+    // asserted uniform: the 64-bit divisions run on the VALU, and a base pointer
+    // derived from them must stay in SGPRs for the LDS-DMA (dma_piece's "s")
+    const int ct0 = __builtin_amdgcn_readfirstlane((int)((int64_t)split * n64 / p.splits));
+    const int ct1 = __builtin_amdgcn_readfirstlane((int)((int64_t)(split + 1) * n64 / p.splits));
     const int ntiles = ct1 - ct0;
     const int64_t q0 = (int64_t)qtile * TILE_Q;
 
-    float* lst_d = (float*)(smem + V5_LD_OFF);
-    int* lst_i = (int*)(smem + V5_LI_OFF);
-    int* cnt = (int*)(smem + V5_CNT_OFF);
-    float* tau = (float*)(smem + V5_TAU_OFF);
+    float* lst_d = (float*)(smem + L::LD_OFF);
+    int* lst_i = (int*)(smem + L::LI_OFF);
+    int* cnt = (int*)(smem + L::CNT_OFF);
+    float* tau = (float*)(smem + L::TAU_OFF);
     const int qf = pr * 32 + h * 16;      // first of the 16 queries this wave finalises
     if (lane < 16) {
         cnt[qf + lane] = 0;
@@ -179,7 +190,7 @@ __global__ __launch_bounds__(V5_THREADS, 1) void k_scan_v5(ScanParams p) {
         const int uc = u < ntiles ? u : (ntiles > 0 ? ntiles - 1 : 0);
         const char* src = h ? (const char*)(p.norms + (int64_t)(ct0 + uc) * V5_TR + pr * 16 + (lane & 3) * 4)
                             : (const char*)(gtp + (lane & 7) * 4);
-        const uint32_t m0 = lds_base + V5_AUX_OFF + (uint32_t)(u & 3) * V5_AUX_B + aux_dst;
+        const uint32_t m0 = lds_base + L::AUX_OFF + (uint32_t)(u & 3) * L::AUX_B + aux_dst;
         uint64_t saved;
         asm volatile(
             "s_mov_b64 %0, exec\n\t"
@@ -194,7 +205,8 @@ __global__ __launch_bounds__(V5_THREADS, 1) void k_scan_v5(ScanParams p) {
     // corpus piece kb (0/1) of stage jp of tile base cb into ring slot `slot`
     auto corpus_piece = [&](auto KB, auto JP, const char* cb, uint32_t slot) {
         constexpr int kb = decltype(KB)::value, jp = decltype(JP)::value;
-        dma_piece<jp * 128 + kb * 64>(voff, cb, lds_base + V5_RING_OFF + slot * V5_STAGE + blk_w + kb * 1024);
+        // NOP 4: hipcc may compute the tile base with v_readfirstlane right here
+        dma_piece<jp * 128 + kb * 64, 4>(voff, cb, lds_base + L::RING_OFF + slot * V5_STAGE + blk_w + kb * 1024);
     };
 
     // prologue: stages 0 .. NS-2 (tiles 0 .. (NS-2)/SPT)
@@ -224,14 +236,16 @@ __global__ __launch_bounds__(V5_THREADS, 1) void k_scan_v5(ScanParams p) {
     const uint32_t gt_lane = (uint32_t)(256 + pr * 128 + h * 64 + (lane & 15) * 4);
     // exchange: wave (pr, h) writes its column 1 (the partner's queries) into the
     // partner's region and reads its own region
-    const uint32_t xw = lds_base + V5_XCH_OFF + (uint32_t)(((pr * 2 + (1 - h)) * 2) * 1024 + lane * 16);
-    const uint32_t xr = lds_base + V5_XCH_OFF + (uint32_t)(((pr * 2 + h) * 2) * 1024 + lane * 16);
+    // (STAG: one round, 4 KiB per destination wave; else two rounds of 2 KiB)
+    constexpr uint32_t XREG = STAG ? 4096 : 2048;
+    const uint32_t xw = lds_base + L::XCH_OFF + (uint32_t)((pr * 2 + (1 - h)) * XREG + lane * 16);
+    const uint32_t xr = lds_base + L::XCH_OFF + (uint32_t)((pr * 2 + h) * XREG + lane * 16);
     unsigned* gt_first = p.gtau + q0 + qf;
 
     asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"(PRO_AFTER0) : "memory");
     __builtin_amdgcn_sched_barrier(0);
     // block (m, h, kb) of slot s at RING + s*STAGE + ((m*2 + h)*2 + kb)*1024
-    const uint32_t rd_h = lds_base + V5_RING_OFF + (uint32_t)(h * 2 * 1024 + lane * 16);
+    const uint32_t rd_h = lds_base + L::RING_OFF + (uint32_t)(h * 2 * 1024 + lane * 16);
     uint32_t rd_addr = rd_h;  // slot 0
     if (ntiles > 0) {
         static_for<M>([&](auto MM) {
@@ -239,6 +253,83 @@ __global__ __launch_bounds__(V5_THREADS, 1) void k_scan_v5(ScanParams p) {
             ds_rd128<m * 4096>(X[m], rd_addr);
         });
     }
+
+    // STAG: this wave's own column of the previous tile (keyt) and its
+    // thresholds wait across the next tile's first barrier; waves 0-3 finish
+    // that tile before their first MFMAs of the next one, waves 4-7 after them,
+    // so each SIMD overlaps one wave's epilogue with its partner's MFMAs
+    // (MI355X_MICROARCH.md "two waves per SIMD", item 9)
+    f32x4 keyt[M];
+    float trp = 0.f;
+    unsigned grp = 0u;
+#pragma unroll
+    for (int m = 0; m < M; ++m) keyt[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto finish = [&](int tt) {
+        f32x4 key[M];
+        {
+            f32x4 o0, o1, o2, o3;  // the partner's partial sums of this wave's queries
+            asm volatile(
+                "ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:1024\n\t"
+                "ds_read_b128 %2, %4 offset:2048\n\tds_read_b128 %3, %4 offset:3072\n\ts_waitcnt lgkmcnt(0)"
+                : "=&v"(o0), "=&v"(o1), "=&v"(o2), "=&v"(o3)
+                : "v"(xr)
+                : "memory");
+            key[0] = keyt[0] + o0;
+            key[1] = keyt[1] + o1;
+            key[2] = keyt[2] + o2;
+            key[3] = keyt[3] + o3;
+        }
+        if (METRIC == L2) {
+            const uint32_t na = lds_base + L::AUX_OFF + (uint32_t)(tt & 3) * L::AUX_B + (uint32_t)(rl0 * 4);
+#pragma unroll
+            for (int m = 0; m < M; ++m) {
+                f32x4 y;
+                asm volatile("ds_read_b128 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)"
+                             : "=v"(y)
+                             : "v"(na), "i"(m * 64)
+                             : "memory");
+                key[m] += y;
+            }
+        }
+        if (p.dbgbuf) {
+            float* keys = (float*)p.dbgbuf;
+            const int64_t ld = (int64_t)p.n_ctiles * TILE_R;
+#pragma unroll
+            for (int m = 0; m < M; ++m)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    keys[(q0 + ql) * ld + (int64_t)(ct0 + tt) * V5_TR + rl0 + 16 * m + i] = key[m][i];
+        }
+        const float tn = qv ? fminf(trp, ord2f(grp)) : -FX_INF;
+        float gmin[M], mn;
+#pragma unroll
+        for (int m = 0; m < M; ++m) gmin[m] = fminf(fminf(key[m][0], key[m][1]), fminf(key[m][2], key[m][3]));
+        mn = fminf(fminf(gmin[0], gmin[1]), fminf(gmin[2], gmin[3]));
+        if (__builtin_amdgcn_ballot_w64(mn <= tn)) {
+            const int trow0 = (ct0 + tt) * V5_TR;
+            const int rlim = p.ntotal < (int64_t)trow0 + V5_TR ? (int)p.ntotal : trow0 + V5_TR;
+            unsigned pend = 0u;
+            bool ovf = false;
+            static_for<M>([&](auto MM) {
+                constexpr int m = decltype(MM)::value;
+                if (__builtin_amdgcn_ballot_w64(gmin[m] <= tn))
+                    ovf |= push4<CAPV>(key[m], m, 15u, tn, ql, trow0 + rl0 + m * 16, rlim, lst_d, lst_i, cnt, pend);
+            });
+            while (__builtin_amdgcn_ballot_w64(ovf)) {
+                compact16<CAPV>(lst_d, lst_i, cnt, tau, gt_first, qf, lane);
+                ovf = false;
+                const float tq = qv ? fminf(tau[ql], tn) : -FX_INF;
+                const unsigned pn = pend;
+                pend = 0u;
+                static_for<M>([&](auto MM) {
+                    constexpr int m = decltype(MM)::value;
+                    const unsigned el = (pn >> (4 * m)) & 15u;
+                    if (__builtin_amdgcn_ballot_w64(el != 0u))
+                        ovf |= push4<CAPV>(key[m], m, el, tq, ql, trow0 + rl0 + m * 16, rlim, lst_d, lst_i, cnt, pend);
+                });
+            }
+        }
+    };
 
     int c = 0;
     for (int t = 0; t < ntiles; ++t) {
@@ -255,6 +346,10 @@ __global__ __launch_bounds__(V5_THREADS, 1) void k_scan_v5(ScanParams p) {
             constexpr int W = 4 + ((j + NS - 3) % SPT == 0) + ((j + NS - 2) % SPT == 0);
             asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(W) : "memory");
             __builtin_amdgcn_sched_barrier(0);
+            if constexpr (STAG && j == 0) {
+                if (t > 0 && h == 0) finish(t - 1);  // waves 0-3: previous tile first
+                __builtin_amdgcn_sched_barrier(0);
+            }
             // ---- kb = 0: X MFMAs; read kb = 1 (Y) of this stage after >= 6 MFMAs
             static_for<M>([&](auto MM) {
                 constexpr int m = decltype(MM)::value;
@@ -273,7 +368,7 @@ __global__ __launch_bounds__(V5_THREADS, 1) void k_scan_v5(ScanParams p) {
             });
             if constexpr (LAST) {
                 ds_rd32<0>(tr, tau_addr);
-                const uint32_t ns = lds_base + V5_AUX_OFF + (uint32_t)(t & 3) * V5_AUX_B + gt_lane;
+                const uint32_t ns = lds_base + L::AUX_OFF + (uint32_t)(t & 3) * L::AUX_B + gt_lane;
                 ds_rd32<0>(gr, ns);
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -298,12 +393,28 @@ __global__ __launch_bounds__(V5_THREADS, 1) void k_scan_v5(ScanParams p) {
                 }
             });
             __builtin_amdgcn_sched_barrier(0);
+            if constexpr (STAG && j == 0) {
+                if (t > 0 && h == 1) finish(t - 1);  // waves 4-7: after this stage's MFMAs
+                __builtin_amdgcn_sched_barrier(0);
+            }
             rd_addr = rd_next;
             c = (int)c1;
         });
 
         // ---- epilogue of tile t ----------------------------------------------
         acc_fence4(acc);
+        if constexpr (STAG) {
+            // hand the partner its column, keep ours; finished during the next tile
+            ds_wr128<0>(xw, acc[0][1]);
+            ds_wr128<1024>(xw, acc[1][1]);
+            ds_wr128<2048>(xw, acc[2][1]);
+            ds_wr128<3072>(xw, acc[3][1]);
+#pragma unroll
+            for (int m = 0; m < M; ++m) keyt[m] = acc[m][0];
+            trp = tr;
+            grp = gr;
+            continue;
+        }
         // exchange the partner column in two rounds (m = 0,1 then 2,3)
         static_for<2>([&](auto RR) {
             constexpr int r = decltype(RR)::value;
@@ -324,7 +435,7 @@ __global__ __launch_bounds__(V5_THREADS, 1) void k_scan_v5(ScanParams p) {
         for (int m = 0; m < M; ++m) key[m] = acc[m][0];
         if (METRIC == L2) {
             // + |y|^2 of this lane's rows (16 m + rl0 .. +3) from the tile's aux slot
-            const uint32_t na = lds_base + V5_AUX_OFF + (uint32_t)(t & 3) * V5_AUX_B + (uint32_t)(rl0 * 4);
+            const uint32_t na = lds_base + L::AUX_OFF + (uint32_t)(t & 3) * L::AUX_B + (uint32_t)(rl0 * 4);
 #pragma unroll
             for (int m = 0; m < M; ++m) {
                 f32x4 y;
@@ -357,10 +468,10 @@ __global__ __launch_bounds__(V5_THREADS, 1) void k_scan_v5(ScanParams p) {
             static_for<M>([&](auto MM) {
                 constexpr int m = decltype(MM)::value;
                 if (__builtin_amdgcn_ballot_w64(gmin[m] <= tn))
-                    ovf |= push4(key[m], m, 15u, tn, ql, trow0 + rl0 + m * 16, rlim, lst_d, lst_i, cnt, pend);
+                    ovf |= push4<CAPV>(key[m], m, 15u, tn, ql, trow0 + rl0 + m * 16, rlim, lst_d, lst_i, cnt, pend);
             });
             while (__builtin_amdgcn_ballot_w64(ovf)) {
-                compact16(lst_d, lst_i, cnt, tau, gt_first, qf, lane);
+                compact16<CAPV>(lst_d, lst_i, cnt, tau, gt_first, qf, lane);
                 ovf = false;
                 const float tq = qv ? fminf(tau[ql], tn) : -FX_INF;
                 const unsigned pn = pend;
@@ -369,20 +480,26 @@ __global__ __launch_bounds__(V5_THREADS, 1) void k_scan_v5(ScanParams p) {
                     constexpr int m = decltype(MM)::value;
                     const unsigned el = (pn >> (4 * m)) & 15u;
                     if (__builtin_amdgcn_ballot_w64(el != 0u))
-                        ovf |= push4(key[m], m, el, tq, ql, trow0 + rl0 + m * 16, rlim, lst_d, lst_i, cnt, pend);
+                        ovf |= push4<CAPV>(key[m], m, el, tq, ql, trow0 + rl0 + m * 16, rlim, lst_d, lst_i, cnt, pend);
                 });
             }
         }
     }
 
+    if constexpr (STAG) {
+        if (ntiles > 0) {  // the last tile: both halves finish it after one barrier
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            finish(ntiles - 1);
+        }
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may outlive the workgroup
     const int64_t obase = ((int64_t)qtile * p.splits + split) * TILE_Q;
     for (int qi = 0; qi < 16; ++qi) {
         const int q = qf + qi;
         if (q0 + q >= p.nq) break;
-        const int cn = min(cnt[q], V5_CAP);
-        float d = lane < cn ? lst_d[q * V5_CAP + lane] : FX_INF;
-        int i = lane < cn ? lst_i[q * V5_CAP + lane] : INT_MAX;
+        const int cn = min(cnt[q], CAPV);
+        float d = lane < cn ? lst_d[q * CAPV + lane] : FX_INF;
+        int i = lane < cn ? lst_i[q * CAPV + lane] : INT_MAX;
         sort64(d, i, lane);
         if (lane < KP) {
             p.cand_d[(obase + q) * KP + lane] = d;
@@ -391,41 +508,44 @@ __global__ __launch_bounds__(V5_THREADS, 1) void k_scan_v5(ScanParams p) {
     }
 }
 
-template <int DT, int METRIC, int KSTEPS>
+template <int DT, int METRIC, int KSTEPS, int STAG>
 static hipError_t scan_v5_t(const ScanParams& p, hipStream_t s) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_scan_v5<DT, METRIC, KSTEPS>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, V5_LDS_BYTES);
+    hipError_t e = hipFuncSetAttribute((const void*)k_scan_v5<DT, METRIC, KSTEPS, STAG>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, V5Lds<STAG>::BYTES);
     if (e != hipSuccess) return e;
     const int grid = p.qt_per_xcd > 0 ? 8 * p.qt_per_xcd * p.splits : p.n_qtiles * p.splits;
-    hipLaunchKernelGGL((k_scan_v5<DT, METRIC, KSTEPS>), dim3(grid), dim3(V5_THREADS), V5_LDS_BYTES, s, p);
+    hipLaunchKernelGGL((k_scan_v5<DT, METRIC, KSTEPS, STAG>), dim3(grid), dim3(V5_THREADS), V5Lds<STAG>::BYTES, s,
+                       p);
     return hipGetLastError();
 }
 
+// STAG (the staggered epilogue) is built for the 2-byte dtypes only
 template <int DT, int METRIC>
-static hipError_t scan5_rows(const ScanParams& p, hipStream_t s, bool* handled) {
+static hipError_t scan5_rows(const ScanParams& p, hipStream_t s, bool stag, bool* handled) {
     *handled = true;
+    constexpr bool S = DT != F32;
     switch (p.row_bytes / 64) {
-        case 8: return scan_v5_t<DT, METRIC, 8>(p, s);
-        case 12: return scan_v5_t<DT, METRIC, 12>(p, s);
-        case 16: return scan_v5_t<DT, METRIC, 16>(p, s);
-        case 24: return scan_v5_t<DT, METRIC, 24>(p, s);
+        case 8: return (S && stag) ? scan_v5_t<DT, METRIC, 8, S>(p, s) : scan_v5_t<DT, METRIC, 8, 0>(p, s);
+        case 12: return (S && stag) ? scan_v5_t<DT, METRIC, 12, S>(p, s) : scan_v5_t<DT, METRIC, 12, 0>(p, s);
+        case 16: return (S && stag) ? scan_v5_t<DT, METRIC, 16, S>(p, s) : scan_v5_t<DT, METRIC, 16, 0>(p, s);
+        case 24: return (S && stag) ? scan_v5_t<DT, METRIC, 24, S>(p, s) : scan_v5_t<DT, METRIC, 24, 0>(p, s);
         default: *handled = false; return hipSuccess;
     }
 }
 
-hipError_t launch_scan_mfma5(int st_dt, int metric, const ScanParams& p, hipStream_t s, bool* handled) {
+hipError_t launch_scan_mfma5(int st_dt, int metric, const ScanParams& p, hipStream_t s, bool stag, bool* handled) {
     if (p.row_bytes % 64 != 0) {
         *handled = false;
         return hipSuccess;
     }
     if (metric == L2) {
-        if (st_dt == F32) return scan5_rows<F32, L2>(p, s, handled);
-        if (st_dt == BF16) return scan5_rows<BF16, L2>(p, s, handled);
-        return scan5_rows<F16, L2>(p, s, handled);
+        if (st_dt == F32) return scan5_rows<F32, L2>(p, s, stag, handled);
+        if (st_dt == BF16) return scan5_rows<BF16, L2>(p, s, stag, handled);
+        return scan5_rows<F16, L2>(p, s, stag, handled);
     }
-    if (st_dt == F32) return scan5_rows<F32, IP>(p, s, handled);
-    if (st_dt == BF16) return scan5_rows<BF16, IP>(p, s, handled);
-    return scan5_rows<F16, IP>(p, s, handled);
+    if (st_dt == F32) return scan5_rows<F32, IP>(p, s, stag, handled);
+    if (st_dt == BF16) return scan5_rows<BF16, IP>(p, s, stag, handled);
+    return scan5_rows<F16, IP>(p, s, stag, handled);
 }
 
 }  // namespace fx

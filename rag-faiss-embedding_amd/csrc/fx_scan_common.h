@@ -26,12 +26,15 @@ __device__ __forceinline__ void static_for(F&& f) {
 // LDS[lds + 16 l].  The instruction offset is added to the LDS address as
 // well (LDS = M0 + OFF + 16 lane), so M0 is set to lds - OFF (>= 0: the ring
 // starts at 4 KiB, OFF < 1.5 KiB).  The s_nop is the M0-write -> LDS-DMA wait
-// state.
-template <int OFF>
+// state; NOP = 4 also covers a base SGPR the compiler has just written with
+// v_readfirstlane (VALU-written SGPR -> VMEM: 5 wait states, which hipcc does
+// not insert in front of inline asm).
+template <int OFF, int NOP = 0>
 __device__ __forceinline__ void dma_piece(uint32_t voff, const char* sbase, uint32_t lds) {
     static_assert(OFF >= 0 && OFF < 4096, "M0 = lds - OFF must not wrap (rings start at >= 4 KiB)");
-    asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, %1 offset:%2" ::"v"(voff), "s"(sbase), "i"(OFF),
-                 "{m0}"(lds - OFF)
+    static_assert(NOP >= 0 && NOP <= 7, "s_nop range");
+    asm volatile("s_nop %3\n\tglobal_load_lds_dwordx4 %0, %1 offset:%2" ::"v"(voff), "s"(sbase), "i"(OFF),
+                 "i"(NOP), "{m0}"(lds - OFF)
                  : "memory");
 }
 // a wave-uniform pointer, asserted so (the "s" operand of dma_piece needs it in

@@ -1,6 +1,6 @@
 #!/bin/bash
 # First GPU session for the opt-in scan variants written without hardware:
-#   * the 8-wave K-split scan (k_scan_v5, FX_SCAN_V5=1),
+#   * the 8-wave K-split scan (k_scan_v5, FX_SCAN_V5=1; =2 staggered epilogue),
 #   * the corpus-partitioned XCD placement (FX_SCAN_MAP=1),
 #   * the split-fp32 scan of fp32 indexes (FX_F32_SPLIT=1),
 #   * the small-batch scan k_scan_q32 (FX_SCAN_Q32=1).
@@ -21,6 +21,8 @@ FX_SCAN_V5=1 timeout -k 10 300 python -u -m pytest tests/test_scan_keys.py -x -v
 FX_SCAN_V5=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 120 --timeout-method thread > "$out/parity_v5.log" 2>&1
 timeout -k 10 300 python -u bench.py --no-cpu > "$out/bench_d_v4.json" 2> "$out/bench_d_v4.err"
 FX_SCAN_V5=1 timeout -k 10 300 python -u bench.py --no-cpu > "$out/bench_d_v5.json" 2> "$out/bench_d_v5.err"
+FX_SCAN_V5=2 timeout -k 10 300 python -u -m pytest tests/test_scan_keys.py -x -v --timeout 120 --timeout-method thread > "$out/keys_v5s.log" 2>&1
+FX_SCAN_V5=2 timeout -k 10 300 python -u bench.py --no-cpu > "$out/bench_d_v5s.json" 2> "$out/bench_d_v5s.err"
 # corpus-partitioned XCD placement (FX_SCAN_MAP=1) with each kernel
 FX_SCAN_MAP=1 timeout -k 10 300 python -u bench.py --no-cpu > "$out/bench_d_v4_map.json" 2> "$out/bench_d_v4_map.err"
 FX_SCAN_MAP=1 FX_SCAN_V5=1 timeout -k 10 300 python -u bench.py --no-cpu > "$out/bench_d_v5_map.json" 2> "$out/bench_d_v5_map.err"

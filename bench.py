@@ -281,6 +281,24 @@ def main():
         "fallback_queries_last_step": fallbacks,
         "roofline": roof,
     }
+    if world == 1:
+        # the reference's call form: host float32 queries in, host D / I out
+        # (PCIe both ways), same index -- reported beside `value`, never as it
+        try:
+            xq_h = xq.float().cpu().numpy()
+            ix.search(xq_h, k)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(3):
+                Dh, Ih = ix.search(xq_h, k)
+            t_h = (time.perf_counter() - t0) / 3
+            out["pcie_inclusive"] = {
+                "value": round(nq / t_h, 2), "unit": "queries/s", "ms_per_step": round(t_h * 1e3, 3),
+                "form": "numpy float32 queries -> host D/I (H2D + search + D2H), 3 steps",
+                "ids_match_device_path": bool((Ih == I.cpu().numpy()).all()),
+            }
+        except Exception as e:  # noqa: BLE001 -- a side measurement never breaks the bench line
+            log("pcie-inclusive leg failed:", e)
     if rank == 0 and not args.no_cpu:
         nthreads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
         extra = cpu_baseline_and_recall(args, n_total, d, k, D, I, nthreads)

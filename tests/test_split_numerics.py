@@ -52,3 +52,31 @@ def test_split_dot_error_within_delta_s():
     assert worst <= DELTA_S, worst
     # the constant is not loose by orders of magnitude either (sanity)
     assert worst > DELTA_S / 1000
+
+
+def test_split_key_within_certification_margin():
+    """The whole scan key of the split path, emulated with sequential fp32
+    accumulation (a worst case for the MFMA chain: every product rounded into
+    a running fp32 sum), against k_prep_queries' margin for F32S:
+    eps = (2 gamma_{3K+1} + u)(M^2 + 2|x|M) + 2 delta_s |x| M,  times 1.0625."""
+    rng = np.random.default_rng(8)
+    u = 2.0 ** -24
+    for d in (128, 384):
+        y = rng.standard_normal((64, d)).astype(np.float32) * np.float32(3.0)
+        x = rng.standard_normal((8, d)).astype(np.float32)
+        xs = (-2.0 * x).astype(np.float32)
+        xh, xl, _ = _split(xs)
+        yh, yl, _ = _split(y)
+        ny = np.add.accumulate((y.astype(np.float32) ** 2), axis=1, dtype=np.float32)[:, -1]   # fp32 norms
+        M = float(np.sqrt(ny.astype(np.float64).max()))
+        K = 3 * d + 1
+        g = K * u / (1 - K * u)
+        for qi in range(x.shape[0]):
+            terms = np.concatenate([xh[qi] * yh, xl[qi] * yh, xh[qi] * yl], axis=1).astype(np.float32)  # exact products
+            acc = ny.copy()
+            for c in range(terms.shape[1]):                       # sequential fp32 chain, srcC = |y|^2
+                acc = (acc + terms[:, c]).astype(np.float32)
+            exact = (y.astype(np.float64) ** 2).sum(1) - 2 * y.astype(np.float64) @ x[qi].astype(np.float64)
+            xn = float(np.linalg.norm(x[qi].astype(np.float64)))
+            eps = ((2 * g + u) * (M * M + 2 * xn * M) + 2 * DELTA_S * xn * M) * 1.0625
+            assert np.abs(acc.astype(np.float64) - exact).max() <= eps

@@ -96,6 +96,17 @@ struct FxIndex {
     // F32S scan image of an fp32 index (FX_F32_SPLIT=1): rows [0, split_rows) are current
     DevBuf split;
     int64_t split_rows = 0;
+    // FX_SEARCH_GRAPH=1: the search of a small host batch (the reference's
+    // one-query call form) replayed as one hipGraph per shape, over pinned
+    // host staging; `gkey` = the shape and every buffer the graph captured
+    hipGraphExec_t gexec = nullptr;
+    std::vector<uint64_t> gkey;
+    bool gfailed = false;
+    void* ghq = nullptr;
+    float* ghD = nullptr;
+    int64_t* ghI = nullptr;
+    int* ghnf = nullptr;
+    size_t ghq_bytes = 0, ghd_n = 0;
     int64_t last_fallbacks = 0;
     // profiling
     bool profile = false;
@@ -208,6 +219,28 @@ void plan_scan(const FxIndex* h, int64_t nq, ScanParams& p) {
     p.splits = best;
 }
 
+// FX_F32_SPLIT=1 on an fp32 index: bring its F32S scan image up to date
+// (rows appended since the last search); *split says whether the scan uses it
+hipError_t update_scan_image(FxIndex* h, bool* split) {
+    const int rb64 = h->row_bytes / 64;
+    const char* split_env = getenv("FX_F32_SPLIT");
+    *split = split_env && atoi(split_env) == 1 && h->dtype == F32 && h->row_bytes % 64 == 0 &&
+             (rb64 == 8 || rb64 == 12 || rb64 == 16 || rb64 == 24);
+    if (!*split) return hipSuccess;
+    hipStream_t s = h->stream();
+    const void* old = h->split.p;
+    hipError_t e = h->split.ensure((size_t)h->cap_rows * h->row_bytes);
+    if (e != hipSuccess) return e;
+    if (h->split.p != old || h->split_rows > h->ntotal) {  // fresh buffer: finite (zero) padding rows
+        e = hipMemsetAsync(h->split.p, 0, h->split.bytes, s);
+        if (e != hipSuccess) return e;
+        h->split_rows = 0;
+    }
+    e = launch_split_rows((const float*)h->codes, h->kdim, h->split_rows, h->ntotal, h->split.p, s);
+    if (e == hipSuccess) h->split_rows = h->ntotal;
+    return e;
+}
+
 int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int k, float* D, int64_t* I,
               int out_mem) {
     hipStream_t s = h->stream();
@@ -227,21 +260,9 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
     // FX_F32_SPLIT=1: scan an fp32 index through its split-bf16 image (F32S:
     // 3 bf16 products per term on the bf16 MFMA pipe instead of fp32 MFMA);
     // the refine and the certification still use the fp32 rows
-    const int rb64 = h->row_bytes / 64;
-    const char* split_env = getenv("FX_F32_SPLIT");
-    const bool split = split_env && atoi(split_env) == 1 && h->dtype == F32 && h->row_bytes % 64 == 0 &&
-                       (rb64 == 8 || rb64 == 12 || rb64 == 16 || rb64 == 24);
+    bool split = false;
+    HIP_TRY(update_scan_image(h, &split));
     const int scan_dt = split ? (int)F32S : h->dtype;
-    if (split) {
-        const void* old = h->split.p;
-        HIP_TRY(h->split.ensure((size_t)h->cap_rows * h->row_bytes));
-        if (h->split.p != old || h->split_rows > h->ntotal) {  // fresh buffer: finite (zero) padding rows
-            HIP_TRY(hipMemsetAsync(h->split.p, 0, h->split.bytes, s));
-            h->split_rows = 0;
-        }
-        HIP_TRY(launch_split_rows((const float*)h->codes, h->kdim, h->split_rows, h->ntotal, h->split.p, s));
-        h->split_rows = h->ntotal;
-    }
     HIP_TRY(launch_prep_queries(qdev, q_dtype, nq, nq_pad, h->d, h->kdim, scan_dt, h->metric, (float*)h->qf32.p,
                                 qop, (float*)h->qeps.p, sqrt((double)h->max_sq), s));
 
@@ -382,6 +403,149 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
     return FX_OK;
 }
 
+// Shape + every device buffer a captured search touches: the graph is valid
+// while all of them are unchanged
+std::vector<uint64_t> graph_key(const FxIndex* h, int64_t nq, int q_dtype, int k) {
+    ScanParams sp;
+    plan_scan(h, nq, sp);
+    const char* se = getenv("FX_F32_SPLIT");
+    return {(uint64_t)nq, (uint64_t)q_dtype, (uint64_t)k, (uint64_t)h->ntotal, (uint64_t)h->id_offset,
+            (uint64_t)__builtin_bit_cast(uint32_t, h->max_sq), (uint64_t)(se ? atoi(se) : 0),
+            (uint64_t)sp.splits, (uint64_t)sp.q32_tiles, (uint64_t)sp.xcd_split, (uint64_t)sp.qt_per_xcd,
+            (uint64_t)(uintptr_t)h->codes, (uint64_t)(uintptr_t)h->norms, (uint64_t)(uintptr_t)h->split.p,
+            (uint64_t)(uintptr_t)h->qin.p, (uint64_t)(uintptr_t)h->qf32.p, (uint64_t)(uintptr_t)h->qop.p,
+            (uint64_t)(uintptr_t)h->qeps.p, (uint64_t)(uintptr_t)h->gtau.p, (uint64_t)(uintptr_t)h->cand_d.p,
+            (uint64_t)(uintptr_t)h->cand_i.p, (uint64_t)(uintptr_t)h->dws.p, (uint64_t)(uintptr_t)h->iws.p,
+            (uint64_t)(uintptr_t)h->flag.p};
+}
+
+void graph_release(FxIndex* h) {
+    if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
+    h->gexec = nullptr;
+    h->gkey.clear();
+}
+
+// Record the stream-ordered search of do_search (host queries, host results,
+// no diagnostics) into h->gexec.  Runs right after a do_search of the same
+// shape, so every workspace is sized and every kernel attribute set.
+hipError_t graph_build(FxIndex* h, int64_t nq, int q_dtype, int k, bool split) {
+    graph_release(h);
+    hipStream_t s = h->stream();
+    const size_t qb = (size_t)nq * h->d * dtype_size(q_dtype), nd = (size_t)nq * k;
+    hipError_t e = hipSuccess;
+    if (qb > h->ghq_bytes) {
+        if (h->ghq) (void)hipHostFree(h->ghq);
+        h->ghq = nullptr;
+        h->ghq_bytes = 0;
+        if ((e = hipHostMalloc(&h->ghq, qb, hipHostMallocDefault)) != hipSuccess) return e;
+        h->ghq_bytes = qb;
+    }
+    if (nd > h->ghd_n) {
+        if (h->ghD) (void)hipHostFree(h->ghD);
+        if (h->ghI) (void)hipHostFree(h->ghI);
+        h->ghD = nullptr;
+        h->ghI = nullptr;
+        h->ghd_n = 0;
+        if ((e = hipHostMalloc((void**)&h->ghD, nd * 4, hipHostMallocDefault)) != hipSuccess) return e;
+        if ((e = hipHostMalloc((void**)&h->ghI, nd * 8, hipHostMallocDefault)) != hipSuccess) return e;
+        h->ghd_n = nd;
+    }
+    if (!h->ghnf && (e = hipHostMalloc((void**)&h->ghnf, 4, hipHostMallocDefault)) != hipSuccess) return e;
+
+    const int scan_dt = split ? (int)F32S : h->dtype;
+    const int64_t nq_pad = round_up(nq, TILE_Q);
+    ScanParams sp;
+    plan_scan(h, nq, sp);
+    sp.codes = split ? (const char*)h->split.p : h->codes;
+    sp.norms = h->norms;
+    sp.ntotal = h->ntotal;
+    sp.row_bytes = h->row_bytes;
+    sp.qop = (const char*)h->qop.p;
+    sp.nq = nq;
+    sp.dbg = 0;
+    sp.gtau = (unsigned*)h->gtau.p;
+    sp.cand_d = (float*)h->cand_d.p;
+    sp.cand_i = (int*)h->cand_i.p;
+    sp.trace = nullptr;
+    sp.dbgbuf = nullptr;
+    int* n_flag = (int*)h->flag.p;
+    RefineParams rp;
+    rp.cand_d = sp.cand_d;
+    rp.cand_i = sp.cand_i;
+    rp.splits = sp.splits;
+    rp.nq = nq;
+    rp.k = k;
+    rp.codes = h->codes;
+    rp.row_bytes = h->row_bytes;
+    rp.kdim = h->kdim;
+    rp.qf32 = (const float*)h->qf32.p;
+    rp.qeps = (const float*)h->qeps.p;
+    rp.id_offset = h->id_offset;
+    rp.D = (float*)h->dws.p;
+    rp.I = (int64_t*)h->iws.p;
+    rp.n_flag = n_flag;
+    rp.flag_list = n_flag + 1;
+    rp.prefetch = sp.q32_tiles > 0 ? 4 : 1;
+
+    if ((e = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal)) != hipSuccess) return e;
+    hipError_t ce = hipMemcpyAsync(h->qin.p, h->ghq, qb, hipMemcpyHostToDevice, s);
+    if (ce == hipSuccess)
+        ce = launch_prep_queries(h->qin.p, q_dtype, nq, nq_pad, h->d, h->kdim, scan_dt, h->metric, (float*)h->qf32.p,
+                                 h->qop.p, (float*)h->qeps.p, sqrt((double)h->max_sq), s);
+    if (ce == hipSuccess)
+        ce = hipMemsetD32Async((hipDeviceptr_t)sp.gtau, 0xff800000u, (size_t)sp.n_qtiles * TILE_Q, s);
+    if (ce == hipSuccess) ce = launch_scan(scan_dt, h->metric, sp, s);
+    if (ce == hipSuccess) ce = hipMemsetAsync(n_flag, 0, 4, s);
+    if (ce == hipSuccess) ce = launch_refine(h->dtype, h->metric, rp, s);
+    if (ce == hipSuccess) ce = hipMemcpyAsync(h->ghD, rp.D, nd * 4, hipMemcpyDeviceToHost, s);
+    if (ce == hipSuccess) ce = hipMemcpyAsync(h->ghI, rp.I, nd * 8, hipMemcpyDeviceToHost, s);
+    if (ce == hipSuccess) ce = hipMemcpyAsync(h->ghnf, n_flag, 4, hipMemcpyDeviceToHost, s);
+    hipGraph_t graph = nullptr;
+    e = hipStreamEndCapture(s, &graph);  // always end the capture: the stream must leave capture mode
+    if (ce != hipSuccess) e = ce;
+    if (e == hipSuccess) e = hipGraphInstantiate(&h->gexec, graph, nullptr, nullptr, 0);
+    if (graph) (void)hipGraphDestroy(graph);
+    if (e != hipSuccess) {
+        h->gexec = nullptr;
+        (void)hipGetLastError();
+        return e;
+    }
+    h->gkey = graph_key(h, nq, q_dtype, k);
+    return hipSuccess;
+}
+
+// Small host batches under FX_SEARCH_GRAPH=1: replay the captured search;
+// on a shape / buffer change run do_search and re-capture.  An uncertified
+// query (rare) re-runs do_search, which owns the exact fallback.
+int graph_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int k, float* D, int64_t* I) {
+    bool split = false;
+    HIP_TRY(update_scan_image(h, &split));
+    if (h->gexec && graph_key(h, nq, q_dtype, k) == h->gkey) {
+        hipStream_t s = h->stream();
+        memcpy(h->ghq, q, (size_t)nq * h->d * dtype_size(q_dtype));
+        HIP_TRY(hipGraphLaunch(h->gexec, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (*h->ghnf == 0) {
+            memcpy(D, h->ghD, (size_t)nq * k * 4);
+            memcpy(I, h->ghI, (size_t)nq * k * 8);
+            h->last_fallbacks = 0;
+            return FX_OK;
+        }
+        return do_search(h, nq, q, q_dtype, FX_MEM_HOST, k, D, I, FX_MEM_HOST);
+    }
+    const int rc = do_search(h, nq, q, q_dtype, FX_MEM_HOST, k, D, I, FX_MEM_HOST);
+    if (rc == FX_OK && !h->gfailed) {
+        const hipError_t e = graph_build(h, nq, q_dtype, k, split);
+        if (e != hipSuccess) {  // stay on do_search for this index
+            h->gfailed = true;
+            if (getenv("FX_SEARCH_GRAPH_VERBOSE")) fprintf(stderr, "fx: search graph capture failed: %s\n", hipGetErrorString(e));
+        } else if (getenv("FX_SEARCH_GRAPH_VERBOSE")) {
+            fprintf(stderr, "fx: search graph captured (nq=%lld k=%d)\n", (long long)nq, k);
+        }
+    }
+    return rc;
+}
+
 }  // namespace
 
 extern "C" {
@@ -443,8 +607,13 @@ void fx_index_free(FxIndex* h) {
         if (h->norms) (void)hipFree(h->norms);
         if (h->max_sq_bits) (void)hipFree(h->max_sq_bits);
         for (DevBuf* b : {&h->qin, &h->qf32, &h->qop, &h->qeps, &h->cand_d, &h->cand_i, &h->dws, &h->iws, &h->flag,
-                          &h->fbc_d, &h->fbc_i, &h->stage, &h->gtau, &h->trace, &h->dbgbuf})
+                          &h->fbc_d, &h->fbc_i, &h->stage, &h->gtau, &h->trace, &h->dbgbuf, &h->split})
             b->release();
+        graph_release(h);
+        if (h->ghq) (void)hipHostFree(h->ghq);
+        if (h->ghD) (void)hipHostFree(h->ghD);
+        if (h->ghI) (void)hipHostFree(h->ghI);
+        if (h->ghnf) (void)hipHostFree(h->ghnf);
         for (auto& pr : h->ev_scan) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
         for (auto& pr : h->ev_merge) (void)hipEventDestroy(pr.second);
         if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
@@ -565,6 +734,10 @@ int fx_index_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_me
         h->last_fallbacks = 0;
         return FX_OK;
     }
+    const char* ge = getenv("FX_SEARCH_GRAPH");
+    if (ge && atoi(ge) == 1 && q_mem == FX_MEM_HOST && out_mem == FX_MEM_HOST && nq <= 64 && !h->profile &&
+        !getenv("FX_SCAN_DBG") && !getenv("FX_SCAN_TRACE") && !getenv("FX_SCAN_CAND") && h->user_stream == nullptr)
+        return graph_search(h, nq, q, q_dtype, k, D, I);
     return do_search(h, nq, q, q_dtype, q_mem, k, D, I, out_mem);
 }
 

@@ -1,0 +1,75 @@
+"""Replayed small-batch search (FX_SEARCH_GRAPH=1): host queries in, host
+results out -- the reference's FAISSVectorStore.search call form
+(faiss_store.py:57-77) -- through one captured hipGraph per shape.
+
+Every replay must equal the oracle; the graph must be rebuilt whenever the
+index or the shape changes (add, reset, another k or nq).  Not yet run on
+hardware: skipped unless FX_TEST_EXPERIMENTAL=1.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import cpu as C
+from tests.test_gpu_parity import assert_parity
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(os.environ.get("FX_TEST_EXPERIMENTAL") != "1",
+                                 reason="graph-replayed search not yet validated on MI355X (FX_TEST_EXPERIMENTAL=1)")]
+
+
+@pytest.fixture(scope="module")
+def fx():
+    from rag_faiss_embedding_amd import _lib, faiss
+    if _lib.device_count() == 0:
+        pytest.fail("no GPU visible: -m gpu tests must run on the MI355X box")
+    return faiss
+
+
+@pytest.mark.parametrize("q32", ["0", "1"])
+def test_graph_replay_matches_oracle(fx, monkeypatch, q32):
+    monkeypatch.setenv("FX_SEARCH_GRAPH", "1")
+    monkeypatch.setenv("FX_SCAN_Q32", q32)
+    rng = np.random.default_rng(11)
+    xb = rng.standard_normal((20_000, 384)).astype(np.float32)
+    ix = fx.IndexFlatL2(384)
+    ix.add(xb[:15_000])
+    for r in (3, 77, 14_999, 5, 3):                   # capture, then replays with new query values
+        D, I = ix.search(xb[r:r + 1], 5)
+        Dr, Ir = C.knn_exact(xb[r:r + 1], xb[:15_000], 5)
+        assert_parity(D, I, Dr, Ir)
+    ix.add(xb[15_000:])                               # ntotal changed: re-capture
+    q = rng.standard_normal((1, 384)).astype(np.float32)
+    for _ in range(2):
+        D, I = ix.search(q, 5)
+        Dr, Ir = C.knn_exact(q, xb, 5)
+        assert_parity(D, I, Dr, Ir)
+    for k in (1, 10, 32):                             # another shape each time
+        D, I = ix.search(q, k)
+        Dr, Ir = C.knn_exact(q, xb, k)
+        assert_parity(D, I, Dr, Ir)
+    qs = rng.standard_normal((17, 384)).astype(np.float32)
+    for _ in range(2):
+        D, I = ix.search(qs, 10)
+        Dr, Ir = C.knn_exact(qs, xb, 10)
+        assert_parity(D, I, Dr, Ir)
+    ix.reset()
+    ix.add(xb[:100])
+    D, I = ix.search(q, 5)
+    Dr, Ir = C.knn_exact(q, xb[:100], 5)
+    assert_parity(D, I, Dr, Ir)
+
+
+def test_graph_store_single_queries(fx, monkeypatch):
+    """FAISSVectorStore-style loop: many single-query calls on one index."""
+    monkeypatch.setenv("FX_SEARCH_GRAPH", "1")
+    rng = np.random.default_rng(12)
+    xb = rng.standard_normal((5000, 128)).astype(np.float32)
+    ix = fx.IndexFlatIP(128)
+    ix.add(xb)
+    from oracle import flat_l2 as F
+    for r in range(0, 5000, 500):
+        D, I = ix.search(xb[r:r + 1], 5)
+        Dr, Ir = F.knn_inner_product(xb[r:r + 1], xb, 5)
+        assert_parity(D, I, Dr, Ir)

@@ -488,6 +488,7 @@ hipError_t graph_build(FxIndex* h, int64_t nq, int q_dtype, int k, bool split) {
     rp.prefetch = sp.q32_tiles > 0 ? 4 : 1;
 
     if ((e = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal)) != hipSuccess) return e;
+    g_graph_capture = true;
     hipError_t ce = hipMemcpyAsync(h->qin.p, h->ghq, qb, hipMemcpyHostToDevice, s);
     if (ce == hipSuccess)
         ce = launch_prep_queries(h->qin.p, q_dtype, nq, nq_pad, h->d, h->kdim, scan_dt, h->metric, (float*)h->qf32.p,
@@ -500,6 +501,7 @@ hipError_t graph_build(FxIndex* h, int64_t nq, int q_dtype, int k, bool split) {
     if (ce == hipSuccess) ce = hipMemcpyAsync(h->ghD, rp.D, nd * 4, hipMemcpyDeviceToHost, s);
     if (ce == hipSuccess) ce = hipMemcpyAsync(h->ghI, rp.I, nd * 8, hipMemcpyDeviceToHost, s);
     if (ce == hipSuccess) ce = hipMemcpyAsync(h->ghnf, n_flag, 4, hipMemcpyDeviceToHost, s);
+    g_graph_capture = false;
     hipGraph_t graph = nullptr;
     e = hipStreamEndCapture(s, &graph);  // always end the capture: the stream must leave capture mode
     if (ce != hipSuccess) e = ce;

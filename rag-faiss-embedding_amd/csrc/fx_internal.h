@@ -81,6 +81,11 @@ struct RefineParams {
     int prefetch;          // > 1: phase-1 loads issued 4 chunks at a time (small-batch scan)
 };
 
+// True on a thread that is capturing a search into a hipGraph (fx_index.cpp
+// graph_build): the scan launchers then skip hipFuncSetAttribute, which the
+// do_search right before the capture has already applied for the same kernel.
+extern thread_local bool g_graph_capture;
+
 // launchers (stream-ordered, no host sync) -- fx_kernels.hip
 hipError_t launch_convert_rows(const void* x, int x_dt, int64_t n, int d, void* codes_row0, int st_dt,
                                int kdim, float* norms_row0, unsigned* max_sq_bits, int normalize,

@@ -32,6 +32,8 @@
 
 namespace fx {
 
+thread_local bool g_graph_capture = false;
+
 // ---------------------------------------------------------------------------
 // add(): convert rows into the code matrix, compute |y|^2
 // ---------------------------------------------------------------------------
@@ -694,7 +696,7 @@ hipError_t launch_prep_queries(const void* q, int q_dt, int64_t nq, int64_t nq_p
 template <int DT, int METRIC>
 static hipError_t scan_t(const ScanParams& p, hipStream_t s) {
     // > 64 KiB of dynamic LDS must be opted into (per device; cheap to repeat)
-    hipError_t e = hipFuncSetAttribute((const void*)k_scan_topk<DT, METRIC>,
+    hipError_t e = g_graph_capture ? hipSuccess : hipFuncSetAttribute((const void*)k_scan_topk<DT, METRIC>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, LDS_SCAN_BYTES);
     if (e != hipSuccess) return e;
     const int grid = p.qt_per_xcd > 0 ? 8 * p.qt_per_xcd * p.splits : p.n_qtiles * p.splits;

@@ -389,7 +389,7 @@ static hipError_t scan_v4_t(const ScanParams& p, hipStream_t s) {
         }
     }
 #endif
-    hipError_t e = hipFuncSetAttribute((const void*)k_scan_v4<DT, METRIC, KSTEPS, ABL>,
+    hipError_t e = g_graph_capture ? hipSuccess : hipFuncSetAttribute((const void*)k_scan_v4<DT, METRIC, KSTEPS, ABL>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, S_LDS_BYTES);
     if (e != hipSuccess) return e;
     const int grid = p.qt_per_xcd > 0 ? 8 * p.qt_per_xcd * p.splits : p.n_qtiles * p.splits;

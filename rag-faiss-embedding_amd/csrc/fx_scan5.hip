@@ -510,7 +510,7 @@ __global__ __launch_bounds__(V5_THREADS, 1) void k_scan_v5(ScanParams p) {
 
 template <int DT, int METRIC, int KSTEPS, int STAG>
 static hipError_t scan_v5_t(const ScanParams& p, hipStream_t s) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_scan_v5<DT, METRIC, KSTEPS, STAG>,
+    hipError_t e = g_graph_capture ? hipSuccess : hipFuncSetAttribute((const void*)k_scan_v5<DT, METRIC, KSTEPS, STAG>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, V5Lds<STAG>::BYTES);
     if (e != hipSuccess) return e;
     const int grid = p.qt_per_xcd > 0 ? 8 * p.qt_per_xcd * p.splits : p.n_qtiles * p.splits;

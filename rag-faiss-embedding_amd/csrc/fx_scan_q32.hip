@@ -332,7 +332,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_q32(ScanParams p) {
 
 template <int DT, int METRIC, int KSTEPS>
 static hipError_t scan_q32_t(const ScanParams& p, hipStream_t s) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_scan_q32<DT, METRIC, KSTEPS>,
+    hipError_t e = g_graph_capture ? hipSuccess : hipFuncSetAttribute((const void*)k_scan_q32<DT, METRIC, KSTEPS>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, Q_LDS_BYTES);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL((k_scan_q32<DT, METRIC, KSTEPS>), dim3(p.q32_tiles * p.splits), dim3(SCAN_THREADS),

@@ -19,7 +19,7 @@ if [ "$stage" = low ]; then
   FX_TEST_EXPERIMENTAL=1 $T 300 $PYT tests/test_f32_split.py > "$out/split.log" 2>&1
   $T 240 python -u bench.py --config b --no-cpu > "$out/bench_b.json" 2> "$out/bench_b.err"
   FX_F32_SPLIT=1 $T 240 python -u bench.py --config b --no-cpu > "$out/bench_b_split.json" 2> "$out/bench_b_split.err"
-  FX_SCAN_MAP=1 $T 300 $PYT tests/test_scan_keys.py > "$out/keys_map.log" 2>&1
+  FX_SCAN_MAP=1 $T 300 $PYT tests/test_gpu_parity.py -k large_synth > "$out/parity_map.log" 2>&1  # >= 32 tiles: MAP active
   $T 300 python -u bench.py --no-cpu > "$out/bench_d_v4.json" 2> "$out/bench_d_v4.err"
   FX_SCAN_MAP=1 $T 300 python -u bench.py --no-cpu > "$out/bench_d_v4_map.json" 2> "$out/bench_d_v4_map.err"
   FX_TEST_EXPERIMENTAL=1 $T 300 $PYT "tests/test_search_graph.py::test_graph_replay_matches_oracle[0]" \

@@ -712,8 +712,13 @@ hipError_t launch_scan(int st_dt, int metric, const ScanParams& p, hipStream_t s
         hipError_t e = launch_scan_q32(st_dt, metric, p, s, &handled);
         return handled ? e : hipErrorInvalidValue;
     }
-    if (st_dt == F32S) {  // the split-fp32 operand exists only for the MFMA scan
+    if (st_dt == F32S) {  // the split-fp32 operand exists only for the MFMA scans
+        static const int v5s = getenv("FX_SCAN_V5") != nullptr ? atoi(getenv("FX_SCAN_V5")) : 0;
         bool handled = false;
+        if (v5s) {
+            hipError_t e = launch_scan_mfma5(st_dt, metric, p, s, v5s == 2, &handled);
+            if (handled) return e;
+        }
         hipError_t e = launch_scan_mfma(st_dt, metric, p, s, &handled);
         return handled ? e : hipErrorInvalidValue;
     }

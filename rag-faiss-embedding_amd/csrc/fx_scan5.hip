@@ -118,8 +118,13 @@ __global__ __launch_bounds__(V5_THREADS, 1) void k_scan_v5(ScanParams p) {
     typedef typename AsmMmaV<DT>::A frag_t;
     typedef typename AsmMmaV<DT>::B bfrag_t;
     static_assert(KSTEPS % 4 == 0, "each half must hold a whole number of 128-B stages");
+    // F32S (split fp32, rows [hi plane | lo plane]): wave half h takes quarter h
+    // of EACH plane, so both halves run hi*x_hi + hi*x_lo + lo*x_hi on equal work
+    constexpr bool SPL = DT == F32S;
+    static_assert(!SPL || KSTEPS % 8 == 0, "F32S: a plane quarter must be whole 128-B stages");
     constexpr int RB = KSTEPS * 64;       // row stride (bytes)
     constexpr int HB = RB / 2;            // bytes of one K half
+    constexpr int QB = RB / 4;            // F32S: bytes of one plane quarter
     constexpr int KH = KSTEPS / 2;        // 64-B K-steps per half
     constexpr int SPT = KSTEPS / 4;       // stages per tile (128 B of each half per stage)
     constexpr int NS = V5_NS;
@@ -159,11 +164,15 @@ __global__ __launch_bounds__(V5_THREADS, 1) void k_scan_v5(ScanParams p) {
         // column n holds queries pr*32 + (n ^ h)*16 ..: column 0 is always the
         // 16 queries this wave finalises, column 1 its partner's (no dynamic
         // register indexing in the epilogue)
-        const char* qb = p.qop + (q0 + pr * 32 + (lane & 15)) * RB + h * HB + (lane >> 4) * 16;
+        // (F32S: K-steps 0 .. KH/2-1 = quarter h of x_hi, KH/2 .. KH-1 = quarter h of x_lo)
+        const char* qb = p.qop + (q0 + pr * 32 + (lane & 15)) * RB + (lane >> 4) * 16;
 #pragma unroll
-        for (int ks = 0; ks < KH; ++ks)
+        for (int ks = 0; ks < KH; ++ks) {
+            const int kofs = !SPL ? h * HB + ks * 64
+                                  : (ks < KH / 2 ? h * QB + ks * 64 : HB + h * QB + (ks - KH / 2) * 64);
 #pragma unroll
-            for (int n = 0; n < N; ++n) b[ks][n] = *(const bfrag_t*)(qb + (n ^ h) * 16 * RB + ks * 64);
+            for (int n = 0; n < N; ++n) b[ks][n] = *(const bfrag_t*)(qb + (n ^ h) * 16 * RB + kofs);
+        }
 #pragma unroll
         for (int ks = 0; ks < KH; ++ks)
 #pragma unroll
@@ -173,7 +182,7 @@ __global__ __launch_bounds__(V5_THREADS, 1) void k_scan_v5(ScanParams p) {
     // ---- DMA: wave w moves LDS blocks (m = pr, h, kb = 0/1) of every stage:
     //      rows 16 pr .. 16 pr + 15, bytes h HB + 128 j + 64 kb of its half
     const uint32_t lds_base = lds_off(smem);
-    const uint32_t voff = (uint32_t)((pr * 16 + (lane & 15)) * RB + h * HB + (lane >> 4) * 16);
+    const uint32_t voff = (uint32_t)((pr * 16 + (lane & 15)) * RB + h * (SPL ? QB : HB) + (lane >> 4) * 16);
     const uint32_t blk_w = (uint32_t)(((pr * 2 + h) * 2) * 1024);   // block (m = pr, h, kb = 0)
     const char* cb0 = p.codes + (int64_t)ct0 * TB;
     const char* cb_last = sgpr_ptr(p.codes + (int64_t)(ct0 + (ntiles > 0 ? ntiles - 1 : 0)) * TB);
@@ -206,7 +215,9 @@ __global__ __launch_bounds__(V5_THREADS, 1) void k_scan_v5(ScanParams p) {
     auto corpus_piece = [&](auto KB, auto JP, const char* cb, uint32_t slot) {
         constexpr int kb = decltype(KB)::value, jp = decltype(JP)::value;
         // NOP 4: hipcc may compute the tile base with v_readfirstlane right here
-        dma_piece<jp * 128 + kb * 64, 4>(voff, cb, lds_base + L::RING_OFF + slot * V5_STAGE + blk_w + kb * 1024);
+        // F32S: stages 0 .. SPT/2-1 walk the hi plane's quarter, the rest the lo plane's
+        constexpr int sofs = !SPL ? jp * 128 : (jp < SPT / 2 ? jp * 128 : HB + (jp - SPT / 2) * 128);
+        dma_piece<sofs + kb * 64, 4>(voff, cb, lds_base + L::RING_OFF + slot * V5_STAGE + blk_w + kb * 1024);
     };
 
     // prologue: stages 0 .. NS-2 (tiles 0 .. (NS-2)/SPT)
@@ -350,11 +361,14 @@ __global__ __launch_bounds__(V5_THREADS, 1) void k_scan_v5(ScanParams p) {
                 if (t > 0 && h == 0) finish(t - 1);  // waves 0-3: previous tile first
                 __builtin_amdgcn_sched_barrier(0);
             }
+            // F32S: hi stages (j < SPT/2) take x_hi then x_lo, lo stages x_hi only
+            constexpr bool HI = SPL && j < SPT / 2;
+            constexpr int kq = (SPL && !HI) ? 2 * (j - SPT / 2) : 2 * j;  // B K-step of half kb = 0
             // ---- kb = 0: X MFMAs; read kb = 1 (Y) of this stage after >= 6 MFMAs
             static_for<M>([&](auto MM) {
                 constexpr int m = decltype(MM)::value;
                 constexpr int INIT = j == 0 ? 2 : 0;  // first K-step of the tile: srcC = 0
-                AsmMmaV<DT>::template mma2<INIT>(acc[m][0], acc[m][1], X[m], b[2 * j][0], b[2 * j][1], acc[m][0]);
+                AsmMmaV<DT>::template mma2<INIT>(acc[m][0], acc[m][1], X[m], b[kq][0], b[kq][1], acc[m][0]);
                 if constexpr (m == 1) {
                     ds_rd128<0 * 4096 + 1024>(Y[0], rd_addr);
                     ds_rd128<1 * 4096 + 1024>(Y[1], rd_addr);
@@ -366,6 +380,13 @@ __global__ __launch_bounds__(V5_THREADS, 1) void k_scan_v5(ScanParams p) {
                 if constexpr (m == 3)
                     corpus_piece(std::integral_constant<int, 0>{}, JP{}, tile_base(t + jq / SPT), c4);
             });
+            if constexpr (HI) {
+                static_for<M>([&](auto MM) {
+                    constexpr int m = decltype(MM)::value;
+                    AsmMmaV<DT>::template mma2<0>(acc[m][0], acc[m][1], X[m], b[KH / 2 + kq][0], b[KH / 2 + kq][1],
+                                                  acc[m][0]);
+                });
+            }
             if constexpr (LAST) {
                 ds_rd32<0>(tr, tau_addr);
                 const uint32_t ns = lds_base + L::AUX_OFF + (uint32_t)(t & 3) * L::AUX_B + gt_lane;
@@ -377,8 +398,7 @@ __global__ __launch_bounds__(V5_THREADS, 1) void k_scan_v5(ScanParams p) {
             const uint32_t rd_next = rd_h + c1 * V5_STAGE;
             static_for<M>([&](auto MM) {
                 constexpr int m = decltype(MM)::value;
-                AsmMmaV<DT>::template mma2<0>(acc[m][0], acc[m][1], Y[m], b[2 * j + 1][0], b[2 * j + 1][1],
-                                              acc[m][0]);
+                AsmMmaV<DT>::template mma2<0>(acc[m][0], acc[m][1], Y[m], b[kq + 1][0], b[kq + 1][1], acc[m][0]);
                 if constexpr (m == 1) {
                     ds_rd128<0 * 4096>(X[0], rd_next);
                     ds_rd128<1 * 4096>(X[1], rd_next);
@@ -392,6 +412,13 @@ __global__ __launch_bounds__(V5_THREADS, 1) void k_scan_v5(ScanParams p) {
                     if constexpr (jq % SPT == 0) aux_piece(t + jq / SPT);
                 }
             });
+            if constexpr (HI) {
+                static_for<M>([&](auto MM) {
+                    constexpr int m = decltype(MM)::value;
+                    AsmMmaV<DT>::template mma2<0>(acc[m][0], acc[m][1], Y[m], b[KH / 2 + kq + 1][0],
+                                                  b[KH / 2 + kq + 1][1], acc[m][0]);
+                });
+            }
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (STAG && j == 0) {
                 if (t > 0 && h == 1) finish(t - 1);  // waves 4-7: after this stage's MFMAs
@@ -526,7 +553,13 @@ static hipError_t scan5_rows(const ScanParams& p, hipStream_t s, bool stag, bool
     constexpr bool S = DT != F32;
     switch (p.row_bytes / 64) {
         case 8: return (S && stag) ? scan_v5_t<DT, METRIC, 8, S>(p, s) : scan_v5_t<DT, METRIC, 8, 0>(p, s);
-        case 12: return (S && stag) ? scan_v5_t<DT, METRIC, 12, S>(p, s) : scan_v5_t<DT, METRIC, 12, 0>(p, s);
+        case 12:
+            if constexpr (DT == F32S) {  // a plane quarter of 192 B is not whole stages: k_scan_v4 takes it
+                *handled = false;
+                return hipSuccess;
+            } else {
+                return (S && stag) ? scan_v5_t<DT, METRIC, 12, S>(p, s) : scan_v5_t<DT, METRIC, 12, 0>(p, s);
+            }
         case 16: return (S && stag) ? scan_v5_t<DT, METRIC, 16, S>(p, s) : scan_v5_t<DT, METRIC, 16, 0>(p, s);
         case 24: return (S && stag) ? scan_v5_t<DT, METRIC, 24, S>(p, s) : scan_v5_t<DT, METRIC, 24, 0>(p, s);
         default: *handled = false; return hipSuccess;
@@ -538,6 +571,8 @@ hipError_t launch_scan_mfma5(int st_dt, int metric, const ScanParams& p, hipStre
         *handled = false;
         return hipSuccess;
     }
+    if (st_dt == F32S)
+        return metric == L2 ? scan5_rows<F32S, L2>(p, s, stag, handled) : scan5_rows<F32S, IP>(p, s, stag, handled);
     if (metric == L2) {
         if (st_dt == F32) return scan5_rows<F32, L2>(p, s, stag, handled);
         if (st_dt == BF16) return scan5_rows<BF16, L2>(p, s, stag, handled);

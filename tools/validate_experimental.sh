@@ -53,5 +53,8 @@ if [ "$stage" = v5 ]; then
   FX_SCAN_V5=2 $T 300 $PYT tests/test_scan_keys.py > "$out/keys_v5s.log" 2>&1
   FX_SCAN_V5=2 $T 300 python -u bench.py --no-cpu > "$out/bench_d_v5s.json" 2> "$out/bench_d_v5s.err"
   FX_SCAN_V5=2 FX_SCAN_MAP=1 $T 300 python -u bench.py --no-cpu > "$out/bench_d_v5s_map.json" 2> "$out/bench_d_v5s_map.err"
+  # split fp32 on the 8-wave scan (quarter of each plane per wave half)
+  FX_SCAN_V5=1 FX_TEST_EXPERIMENTAL=1 $T 300 $PYT tests/test_f32_split.py > "$out/split_v5.log" 2>&1
+  FX_SCAN_V5=1 FX_F32_SPLIT=1 $T 240 python -u bench.py --config b --no-cpu > "$out/bench_b_split_v5.json" 2> "$out/bench_b_split_v5.err"
 fi
 echo "stage $stage done"

@@ -20,9 +20,13 @@
 //   epilogue: wave (p, h) finalises queries 32p + 16h .. +15 (its column 0):
 //     its own partial + the partner's (2 LDS rounds of 16 KiB) + |y|^2 (L2), then the
 //     group-ballot push of k_scan_v4 into its own 16 LDS lists.
+//   STAG = 1 (FX_SCAN_V5=2): one 32 KiB exchange round at tile end; waves 0-3
+//     finish the tile before the next tile's first MFMAs, waves 4-7 after
+//     them, so each SIMD runs one wave's epilogue beside its partner's MFMAs.
+//   DT = F32S (split fp32): half h takes quarter h of each [hi | lo] plane.
 //
-// Not yet measured on hardware: selected only with FX_SCAN_V5=1 (the product
-// path is k_scan_v4).
+// Not yet measured on hardware: selected only with FX_SCAN_V5=1 / 2 (the
+// product path is k_scan_v4).
 #include "fx_scan_common.h"
 
 #include <stdlib.h>

@@ -55,7 +55,17 @@ static_assert(S_LDS_BYTES <= 160 * 1024, "LDS budget");
 // the product): 1 L2-resident corpus, 2 no corpus DMA, 4 no MFMA, 8 no
 // epilogue, 16 no per-stage barrier, 32 no mid-stage LDS wait -- timing only,
 // results invalid
-template <int DT, int METRIC, int KSTEPS, int ABL = 0>
+//
+// LN selects the shape of the corpus LDS-DMA pieces and of the LDS image:
+//   LN = 0: fragment-shaped pieces (16 rows x 64 B: each piece touches 16
+//           half cache lines), fragment-ordered image (1 KiB = one A fragment
+//           in lane order);
+//   LN = 1: full-line pieces (8 rows x 128 B: 8 whole lines, half the TA
+//           work per piece), row-linear image with the 16-B chunks of row r
+//           XOR-swizzled by (r & 7) -- the swizzle is applied to the SOURCE
+//           address (LDS-DMA writes lane-linearly), and the fragment reads
+//           undo it, conflict-free for both K halves.
+template <int DT, int METRIC, int KSTEPS, int ABL = 0, int LN = 0>
 __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     typedef typename AsmMmaV<DT>::A frag_t;
@@ -107,7 +117,10 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
     // ---- DMA addressing: scalar tile bases, fixed per-lane offsets ----------
     // piece jj of a wave = LDS block (wave*4 + jj) = 16-row block 2*wave + jj/2,
     // 64-B half jj%2 of the stage's 128 B (fragment-ordered image)
-    const uint32_t voffA = (uint32_t)((2 * wave * 16 + (lane & 15)) * RB + (lane >> 4) * 16);
+    // LN = 1: piece jj of a wave = rows 8 (4 wave + jj) .. +7, lane l -> row
+    // + (l >> 3), source chunk (l & 7) ^ (l >> 3) (= its row & 7)
+    const uint32_t voffA = LN ? (uint32_t)((32 * wave + (lane >> 3)) * RB + (((lane & 7) ^ (lane >> 3)) << 4))
+                              : (uint32_t)((2 * wave * 16 + (lane & 15)) * RB + (lane >> 4) * 16);
     const uint32_t voffB = voffA + 16 * RB;
     const uint32_t lds_base = lds_off(smem);
     const uint32_t m0w = lds_base + S_RING_OFF + wave * 4096;
@@ -125,6 +138,10 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
         const char* cb = decltype(NXT)::value ? cb_nxt : cb_cur;
         const uint32_t m0 = m0w + slot * S_STAGE + w * 1024;
         if constexpr (w < 4 && (ABL & 2)) return;  // ablation: no corpus DMA (results invalid)
+        if constexpr (LN && w < 4) {
+            dma_piece<jp * STAGE_B>(voffA, cb + w * 8 * RB, m0);
+            return;
+        }
         if constexpr (w == 0) dma_piece<jp * STAGE_B>(voffA, cb, m0);
         if constexpr (w == 1) dma_piece<jp * STAGE_B + 64>(voffA, cb, m0);
         if constexpr (w == 2) dma_piece<jp * STAGE_B>(voffB, cb, m0);
@@ -163,7 +180,14 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
 
     asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");  // stage 0 (5 pieces) landed
     __builtin_amdgcn_sched_barrier(0);
-    uint32_t rd_addr = lds_base + S_RING_OFF + (uint32_t)lane * 16;  // slot 0
+    // fragment-read lane offset within a stage slot (half 0); half 1 is at
+    // + rd_h1 (LN = 0: the next 1 KiB block; LN = 1: chunk + 4 under the
+    // swizzle, i.e. byte offset ^ 64)
+    const uint32_t rd_lane = LN ? (uint32_t)((lane & 15) * 128 + ((((lane >> 4)) ^ (lane & 7)) << 4))
+                                : (uint32_t)lane * 16;
+    const uint32_t rd_h1 = LN ? (uint32_t)((lane & 15) * 128 + ((((lane >> 4) + 4) ^ (lane & 7)) << 4)) - rd_lane
+                              : 1024u;
+    uint32_t rd_addr = lds_base + S_RING_OFF + rd_lane;  // slot 0
     if (ntiles > 0) {
         static_for<M>([&](auto MM) {
             constexpr int m = decltype(MM)::value;
@@ -217,8 +241,9 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                 // half 1 of this stage: two reads per pair over the first four
                 // pairs, so the mid-stage wait finds them landed
                 if constexpr (m < M / 2) {
-                    ds_rd128<(2 * m) * 2048 + 1024>(Y[2 * m], rd_addr);
-                    ds_rd128<(2 * m + 1) * 2048 + 1024>(Y[2 * m + 1], rd_addr);
+                    const uint32_t rd1 = rd_addr + rd_h1;
+                    ds_rd128<(2 * m) * 2048>(Y[2 * m], rd1);
+                    ds_rd128<(2 * m + 1) * 2048>(Y[2 * m + 1], rd1);
                 }
                 if constexpr (LAST && m >= M / 2) {
                     // the next tile's row norms (its first MFMAs' srcC)
@@ -248,7 +273,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
             if constexpr (!(ABL & 32)) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
             // ---- half 1: Y MFMAs; read half 0 (X) of stage g+1 meanwhile
-            const uint32_t rd_next = lds_base + S_RING_OFF + c1 * S_STAGE + (uint32_t)lane * 16;
+            const uint32_t rd_next = lds_base + S_RING_OFF + c1 * S_STAGE + rd_lane;
             static_for<M>([&](auto MM) {
                 constexpr int m = decltype(MM)::value;
                 if constexpr (!(ABL & 4))
@@ -370,30 +395,37 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
     if (p.trace && tid == 0) p.trace[blockIdx.x * 4 + 3] = wall_clock64();
 }
 
-template <int DT, int METRIC, int KSTEPS, int ABL = 0>
+template <int DT, int METRIC, int KSTEPS, int ABL = 0, int LN = 0>
 static hipError_t scan_v4_t(const ScanParams& p, hipStream_t s) {
+    // full-line pieces are the default; FX_SCAN_LINE=0 selects the
+    // fragment-shaped pieces of round 1 (A/B only)
+    if constexpr (ABL == 0 && LN == 0) {
+        static const int ln = getenv("FX_SCAN_LINE") ? atoi(getenv("FX_SCAN_LINE")) : 1;
+        if (ln != 0) return scan_v4_t<DT, METRIC, KSTEPS, 0, 1>(p, s);
+    }
 #ifdef FX_ABLATION
     if constexpr (ABL == 0 && DT == BF16 && METRIC == L2 && KSTEPS == 24) {
         switch (p.dbg & 63) {
-            case 1: return scan_v4_t<DT, METRIC, KSTEPS, 1>(p, s);
-            case 2: return scan_v4_t<DT, METRIC, KSTEPS, 2>(p, s);
-            case 4: return scan_v4_t<DT, METRIC, KSTEPS, 4>(p, s);
-            case 8: return scan_v4_t<DT, METRIC, KSTEPS, 8>(p, s);
-            case 10: return scan_v4_t<DT, METRIC, KSTEPS, 10>(p, s);
-            case 14: return scan_v4_t<DT, METRIC, KSTEPS, 14>(p, s);
-            case 26: return scan_v4_t<DT, METRIC, KSTEPS, 26>(p, s);
-            case 42: return scan_v4_t<DT, METRIC, KSTEPS, 42>(p, s);
-            case 58: return scan_v4_t<DT, METRIC, KSTEPS, 58>(p, s);
-            case 16: return scan_v4_t<DT, METRIC, KSTEPS, 16>(p, s);
+            case 1: return scan_v4_t<DT, METRIC, KSTEPS, 1, LN>(p, s);
+            case 2: return scan_v4_t<DT, METRIC, KSTEPS, 2, LN>(p, s);
+            case 4: return scan_v4_t<DT, METRIC, KSTEPS, 4, LN>(p, s);
+            case 8: return scan_v4_t<DT, METRIC, KSTEPS, 8, LN>(p, s);
+            case 10: return scan_v4_t<DT, METRIC, KSTEPS, 10, LN>(p, s);
+            case 14: return scan_v4_t<DT, METRIC, KSTEPS, 14, LN>(p, s);
+            case 26: return scan_v4_t<DT, METRIC, KSTEPS, 26, LN>(p, s);
+            case 42: return scan_v4_t<DT, METRIC, KSTEPS, 42, LN>(p, s);
+            case 58: return scan_v4_t<DT, METRIC, KSTEPS, 58, LN>(p, s);
+            case 16: return scan_v4_t<DT, METRIC, KSTEPS, 16, LN>(p, s);
             default: break;
         }
     }
 #endif
-    hipError_t e = g_graph_capture ? hipSuccess : hipFuncSetAttribute((const void*)k_scan_v4<DT, METRIC, KSTEPS, ABL>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, S_LDS_BYTES);
+    hipError_t e = g_graph_capture ? hipSuccess
+                                   : hipFuncSetAttribute((const void*)k_scan_v4<DT, METRIC, KSTEPS, ABL, LN>,
+                                                         hipFuncAttributeMaxDynamicSharedMemorySize, S_LDS_BYTES);
     if (e != hipSuccess) return e;
     const int grid = p.qt_per_xcd > 0 ? 8 * p.qt_per_xcd * p.splits : p.n_qtiles * p.splits;
-    hipLaunchKernelGGL((k_scan_v4<DT, METRIC, KSTEPS, ABL>), dim3(grid), dim3(SCAN_THREADS), S_LDS_BYTES, s, p);
+    hipLaunchKernelGGL((k_scan_v4<DT, METRIC, KSTEPS, ABL, LN>), dim3(grid), dim3(SCAN_THREADS), S_LDS_BYTES, s, p);
     return hipGetLastError();
 }
 

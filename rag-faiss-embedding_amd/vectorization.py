@@ -10,20 +10,26 @@ MI355X changes:
 * ``generate_embeddings_device`` returns the embeddings as one device tensor
   (no per-batch ``.cpu().numpy()`` sync at vectorization.py:44) so they can be
   handed straight to ``IndexFlatL2.add`` / ``FAISSVectorStore.add_vectors``;
-* batches are length-bucketed (sorted by token count) and run under bf16
-  autocast on the GPU (``precision="fp32"`` keeps the reference arithmetic).
+* batches are length-bucketed (sorted by token count).  The default
+  ``precision="fp32"`` keeps the reference arithmetic (vectorization.py:41-44
+  runs the fp32 forward); ``precision="bf16"`` (bf16 autocast) is opt-in.
 
-Offline note: the checkpoint ``sentence-transformers/all-MiniLM-L6-v2`` cannot
-be downloaded in this environment.  When it is not in the local HF cache the
-pipeline builds the same architecture (BertModel: 6 layers, hidden 384, 12
-heads, FFN 1536, vocab 30522) with seeded random weights and a deterministic
-hashing tokenizer, so throughput and the device hand-off are faithful while
-embedding VALUES are not the checkpoint's ("parity unpinned").
+Checkpoint loading follows the reference: ``from_pretrained`` failing raises
+(vectorization.py:12-13 let the exception propagate).  The checkpoint
+``sentence-transformers/all-MiniLM-L6-v2`` cannot be downloaded in this
+environment, so benches and tests opt in to a stand-in with
+``allow_random_init=True`` (or ``FX_ALLOW_RANDOM_ENCODER=1``): the same
+architecture (BertModel: 6 layers, hidden 384, 12 heads, FFN 1536, vocab
+30522) with seeded random weights and a deterministic hashing tokenizer, so
+throughput and the device hand-off are faithful while embedding VALUES are not
+the checkpoint's ("parity unpinned").  A WARNING is logged whenever
+the stand-in is active.
 """
 from __future__ import annotations
 
 import hashlib
 import logging
+import os
 import re
 from typing import Dict, List, Optional
 
@@ -67,15 +73,26 @@ class HashingTokenizer:
         return {"input_ids": ids, "token_type_ids": torch.zeros_like(ids), "attention_mask": mask}
 
 
-def build_encoder(model_name: str, seed: int = 0):
-    """(tokenizer, model, pretrained?) -- the real checkpoint when it is in the
-    local HF cache, otherwise the MiniLM architecture with seeded weights."""
+def random_init_allowed(flag: Optional[bool] = None) -> bool:
+    if flag is not None:
+        return bool(flag)
+    return os.environ.get("FX_ALLOW_RANDOM_ENCODER", "0") not in ("", "0")
+
+
+def build_encoder(model_name: str, seed: int = 0, allow_random_init: Optional[bool] = None):
+    """(tokenizer, model, pretrained?) -- the checkpoint from the local HF
+    cache.  If it cannot be loaded the error propagates, as in the reference,
+    unless the seeded random-weight stand-in was asked for explicitly."""
     from transformers import AutoModel, AutoTokenizer, BertConfig, BertModel
     try:
         tok = AutoTokenizer.from_pretrained(model_name, local_files_only=True)
         model = AutoModel.from_pretrained(model_name, local_files_only=True)
         return tok, model, True
-    except Exception:  # noqa: BLE001 -- offline: no checkpoint
+    except Exception as e:  # noqa: BLE001
+        if not random_init_allowed(allow_random_init):
+            raise
+        logger.warning("checkpoint %s unavailable (%s: %s); using the seeded random-weight MiniLM stand-in "
+                       "(embedding values are NOT the checkpoint's)", model_name, type(e).__name__, e)
         torch.manual_seed(seed)
         cfg = BertConfig(**MINILM_CONFIG)
         try:
@@ -87,8 +104,10 @@ def build_encoder(model_name: str, seed: int = 0):
 
 class VectorizationPipeline:
     def __init__(self, model_name: str = "sentence-transformers/all-MiniLM-L6-v2", *, device: Optional[str] = None,
-                 precision: str = "bf16", seed: int = 0):
-        self.tokenizer, self.model, self.pretrained = build_encoder(model_name, seed)
+                 precision: str = "fp32", seed: int = 0, allow_random_init: Optional[bool] = None):
+        if precision not in ("fp32", "bf16"):
+            raise ValueError(f"precision must be 'fp32' or 'bf16', got {precision!r}")
+        self.tokenizer, self.model, self.pretrained = build_encoder(model_name, seed, allow_random_init)
         self.device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
         self.model.to(self.device).eval()
         self.precision = precision if self.device.type == "cuda" else "fp32"

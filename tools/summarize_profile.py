@@ -46,7 +46,7 @@ def main():
             kern[r["Name"]] = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6,
                                "pct": float(r["Percentage"])}
     pmc = {}
-    for sub in ("fetch", "write", "tcc", "sq"):
+    for sub in ("fetch", "write", "tcc", "sq", "lds", "ta"):
         for name, cs in counters(prof / sub / "run_counter_collection.csv").items():
             if SCAN in name:
                 for c, vals in cs.items():
@@ -69,6 +69,10 @@ def main():
         res["effective_clock_ghz"] = per_xcd / (kern[scan_name]["avg_ms"] * 1e6)
     if "SQ_WAIT_ANY" in pmc:
         res["wave_wait_frac"] = pmc["SQ_WAIT_ANY"] / pmc["SQ_WAVE_CYCLES"]
+        res["wave_issue_stall_frac"] = pmc["SQ_WAIT_INST_ANY"] / pmc["SQ_WAVE_CYCLES"]
+        res["wave_active_frac"] = pmc["SQ_ACTIVE_INST_ANY"] / pmc["SQ_WAVE_CYCLES"]
+    if "SQ_LDS_BANK_CONFLICT" in pmc and pmc.get("SQ_LDS_IDX_ACTIVE"):
+        res["lds_bank_conflict_frac"] = pmc["SQ_LDS_BANK_CONFLICT"] / pmc["SQ_LDS_IDX_ACTIVE"]
     (out / f"{rnd}_{tag}_summary.json").write_text(json.dumps(res, indent=1))
     if "hbm_bytes_per_launch" in res:
         (out / f"pmc_scan_{tag}.json").write_text(json.dumps(

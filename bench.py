@@ -236,7 +236,7 @@ def main():
     t_scan = scan_avg_ms / 1e3
     mfma_tf = flops / t_scan / 1e12
     peak = MFMA_PEAK[dtype]
-    split = dtype == "float32" and os.environ.get("FX_F32_SPLIT") == "1"
+    split = dtype == "float32" and os.environ.get("FX_F32_SPLIT", "1") != "0"
     if split:  # fp32 index scanned as 3 bf16 products per term (fx_scan.hip F32S)
         peak = MFMA_PEAK["bfloat16"] / 3.0
     ridge = peak * 1e12 / (HBM_PEAK_GBS * 1e9)
@@ -248,10 +248,10 @@ def main():
         roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(gbs / HBM_PEAK_GBS, 4)}
     # the committed PMC pass measured the default scan: no traffic figure for an opt-in variant
-    variant = any(os.environ.get(v, "0") != "0" for v in ("FX_SCAN_V5", "FX_SCAN_MAP", "FX_SCAN_Q32", "FX_F32_SPLIT"))
+    variant = (os.environ.get("FX_SCAN_Q32", "0") != "0" or os.environ.get("FX_F32_SPLIT", "1") == "0"
+               or os.environ.get("FX_SCAN_LINE", "1") == "0")
     roof["traffic"] = None if variant else read_pmc_traffic(args.config, n_local, nq)
-    scan_kernel = ("k_scan_q32" if os.environ.get("FX_SCAN_Q32") == "1" and nq <= 32 else
-                   "k_scan_v5" if os.environ.get("FX_SCAN_V5") in ("1", "2") and not split else "k_scan_v4")
+    scan_kernel = "k_scan_q32" if os.environ.get("FX_SCAN_Q32") == "1" and nq <= 32 else "k_scan_v4"
     roof["kernel"] = scan_kernel + \
         (" F32S (fp32 as 3 bf16 MFMA products)" if split else "") + " (fused MFMA distance GEMM + top-k select)"
     roof["kernel_ms_avg"] = round(scan_avg_ms, 4)

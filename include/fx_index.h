@@ -60,8 +60,11 @@ enum {
     FX_E_OOM = -5
 };
 
-/* Maximum k served by fx_index_search (per query). */
-#define FX_MAX_K 32
+/* Maximum k served by fx_index_search (per query).  faiss's CPU
+ * IndexFlatL2::search has no k cap (faiss_store.py:49,64 pass the caller's
+ * k); k <= 32 takes the fused scan's fixed candidate lists, larger k a
+ * block top-K refine without cross-split pruning. */
+#define FX_MAX_K 1024
 
 const char* fx_last_error(void);
 int fx_device_count(int* out);
@@ -92,19 +95,25 @@ int fx_index_metric(const FxIndex* index, int* out);
 int fx_index_reserve(FxIndex* index, int64_t n);
 
 /* index.add(x) (faiss_store.py:46): append n rows of x[n][d] (row-major,
- * dtype x_dtype, host or device); rows get ids ntotal .. ntotal+n-1. */
+ * dtype x_dtype, host or device); rows get ids ntotal .. ntotal+n-1.
+ * With FX_MEM_DEVICE it is stream-ordered (returns without waiting for the
+ * device, unless the code matrix has to grow). */
 int fx_index_add(FxIndex* index, int64_t n, const void* x, int x_dtype, int x_mem);
 
 /* index.search(x, k) (faiss_store.py:64): q[nq][d] -> D[nq][k] (f32),
  * I[nq][k] (int64), out buffers caller-allocated on out_mem.  1 <= k <=
  * FX_MAX_K.  Blocks until results are in host memory when out_mem is
- * FX_MEM_HOST; with FX_MEM_DEVICE it is stream-ordered (no host sync). */
+ * FX_MEM_HOST; with FX_MEM_DEVICE (queries and results on the device) it
+ * is stream-ordered: it enqueues its work and returns without waiting for
+ * the device (the exact fallback for uncertified queries is decided on the
+ * device).  Workspace growth (first search of a larger shape) may
+ * synchronise through hipMalloc / hipFree. */
 int fx_index_search(FxIndex* index, int64_t nq, const void* q, int q_dtype, int q_mem,
                     int k, float* D, int64_t* I, int out_mem);
 
 /* Number of queries of the last search whose top-k could not be certified
  * from the candidate margin and were re-ranked by the exact scan fallback
- * (synchronises the index stream). */
+ * (after an FX_MEM_DEVICE search this synchronises the index stream). */
 int fx_index_last_fallbacks(FxIndex* index, int64_t* out);
 
 /* IndexFlatL2 reset (faiss_store.py:124-128). Keeps the HBM allocation. */

@@ -122,16 +122,8 @@ __device__ __forceinline__ void glds16(const void* gsrc, char* lds_uniform) {
 // in that XCD's L2) and all groups walk the corpus splits in the same order
 // (corpus rows are fetched from HBM about once and re-read from L2/MALL).
 // Placement only changes speed, never results.
-// Alternative (xcd_split > 0, FX_SCAN_MAP=1): XCD x owns a 1/8 slice of the
-// corpus for ALL query tiles and walks it query-tile-major, so the ~32 blocks
-// resident on one XCD stream the SAME split side by side (one fetch per round,
-// L2 hits for the others): corpus traffic ~ n_qtiles/32 x corpus.
 __device__ __forceinline__ void map_block(int b, const ScanParams& p, int& qtile, int& split) {
-    if (p.xcd_split > 0) {
-        const int xcd = b & 7, j = b >> 3;
-        qtile = j % p.n_qtiles;
-        split = xcd * p.xcd_split + j / p.n_qtiles;
-    } else if (p.qt_per_xcd > 0) {
+    if (p.qt_per_xcd > 0) {
         int xcd = b & 7, j = b >> 3;
         qtile = xcd + 8 * (j % p.qt_per_xcd);
         split = j / p.qt_per_xcd;
@@ -160,6 +152,107 @@ __device__ __forceinline__ unsigned f2ord(float f) {
 }
 __device__ __forceinline__ float ord2f(unsigned o) {
     return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
+}
+
+// ---------------------------------------------------------------------------
+// block-wide (256 threads) top-K in LDS for any K <= FX_BIG_K: the paths that
+// are not the fused scan's fixed KP = 32 lists (k > KP refine, the exact
+// fallback, the k > 64 shard merge).  A candidate buffer of B = pow2 >= K +
+// 256 (key, id) pairs; each round every thread offers at most one candidate
+// that beats the running K-th (ties -> smaller id); before a round could
+// overflow the buffer it is bitonic-sorted and cut to its K best.
+// ---------------------------------------------------------------------------
+constexpr int BT_THREADS = 256;
+constexpr int BT_MAXK = 2 * FX_BIG_K;  // largest K of a block top-K (k_refine_big's K1)
+constexpr int BT_MAXB = 4096;          // pow2 >= BT_MAXK + BT_THREADS
+
+template <typename Id>
+struct BtState {  // in LDS
+    int cnt;
+    int total;  // valid candidates offered so far
+    float thr;
+    Id thr_i;
+};
+
+template <typename Id> __device__ __forceinline__ Id bt_none();
+template <> __device__ __forceinline__ int bt_none<int>() { return INT_MAX; }
+template <> __device__ __forceinline__ long long bt_none<long long>() { return LLONG_MAX; }
+
+__device__ __forceinline__ int bt_cap(int K) {
+    int b = 256;
+    while (b < K + BT_THREADS) b <<= 1;
+    return b;
+}
+
+template <typename Id>
+__device__ __forceinline__ void bt_init(BtState<Id>* st) {
+    if (threadIdx.x == 0) {
+        st->cnt = 0;
+        st->total = 0;
+        st->thr = FX_INF;
+        st->thr_i = bt_none<Id>();
+    }
+    __syncthreads();
+}
+
+// ascending bitonic sort of (d, i)[0, n), n a power of two, all 256 threads
+template <typename Id>
+__device__ __forceinline__ void bt_sort(float* d, Id* i, int n) {
+    for (int size = 2; size <= n; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            __syncthreads();
+            for (int t = threadIdx.x; t < n / 2; t += BT_THREADS) {
+                const int lo = (t / stride) * 2 * stride + (t % stride), hi = lo + stride;
+                const bool asc = (lo & size) == 0;
+                const float dl = d[lo], dh = d[hi];
+                const Id il = i[lo], ih = i[hi];
+                if (asc ? key_lt(dh, ih, dl, il) : key_lt(dl, il, dh, ih)) {
+                    d[lo] = dh;
+                    d[hi] = dl;
+                    i[lo] = ih;
+                    i[hi] = il;
+                }
+            }
+        }
+    }
+    __syncthreads();
+}
+
+// sort the buffer and keep its K best; afterwards d/i[0, cnt) is ascending
+template <typename Id>
+__device__ __forceinline__ void bt_flush(float* d, Id* i, BtState<Id>* st, int K, int B) {
+    __syncthreads();
+    const int c = st->cnt;
+    for (int t = c + threadIdx.x; t < B; t += BT_THREADS) {
+        d[t] = FX_INF;
+        i[t] = bt_none<Id>();
+    }
+    bt_sort(d, i, B);
+    if (threadIdx.x == 0) {
+        st->cnt = c < K ? c : K;
+        if (c >= K) {
+            st->thr = d[K - 1];
+            st->thr_i = i[K - 1];
+        }
+    }
+    __syncthreads();
+}
+
+// one round: every thread offers (key, id) when `valid`; call with all 256
+// threads; flushes first when the round could overflow
+template <typename Id>
+__device__ __forceinline__ void bt_round(float* d, Id* i, BtState<Id>* st, int K, int B, float key, Id id,
+                                         bool valid) {
+    __syncthreads();
+    if (st->cnt > B - BT_THREADS) bt_flush(d, i, st, K, B);
+    if (valid) {
+        atomicAdd(&st->total, 1);
+        if (key_lt(key, id, st->thr, st->thr_i)) {
+            const int pos = atomicAdd(&st->cnt, 1);
+            d[pos] = key;
+            i[pos] = id;
+        }
+    }
 }
 
 // Compact every full list (cnt >= CAP) to its KP best entries; tau = KP-th.

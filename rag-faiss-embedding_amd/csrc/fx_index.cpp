@@ -88,12 +88,12 @@ struct FxIndex {
     char* codes = nullptr;
     float* norms = nullptr;
     unsigned* max_sq_bits = nullptr;  // device
-    float max_sq = 0.0f;              // host mirror
     hipStream_t own_stream = nullptr;
     hipStream_t user_stream = nullptr;
     // search workspace
     DevBuf qin, qf32, qop, qeps, cand_d, cand_i, dws, iws, flag, fbc_d, fbc_i, stage, gtau, trace, dbgbuf;
-    // F32S scan image of an fp32 index (FX_F32_SPLIT=1): rows [0, split_rows) are current
+    // F32S scan image of an fp32 index (default; FX_F32_SPLIT=0 scans the fp32
+    // rows with fp32 MFMA instead): rows [0, split_rows) are current
     DevBuf split;
     int64_t split_rows = 0;
     // FX_SEARCH_GRAPH=1: the search of a small host batch (the reference's
@@ -108,6 +108,10 @@ struct FxIndex {
     int* ghnf = nullptr;
     size_t ghq_bytes = 0, ghd_n = 0;
     int64_t last_fallbacks = 0;
+    // uncertified count of the last search, copied stream-ordered into pinned
+    // memory; read (after a stream sync) only when asked for (fb_pending)
+    int* pin_nf = nullptr;
+    bool fb_pending = false;
     // profiling
     bool profile = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_scan, ev_merge;
@@ -158,46 +162,24 @@ hipError_t grow(FxIndex* h, int64_t need_rows) {
 
 // choose corpus splits per query tile: enough workgroups to fill 256 CUs
 // several times over (1 workgroup per CU resident: 129 KiB LDS)
-void plan_scan(const FxIndex* h, int64_t nq, ScanParams& p) {
+// k > KP: no cross-split pruning (ScanParams.share = 0) and at least k/4
+// splits, so that a split's KP-list rarely holds fewer than all of its top-k
+// rows and the certification bound (the smallest full split's KP-th key)
+// lies far beyond the k-th distance
+void plan_scan(const FxIndex* h, int64_t nq, int k, ScanParams& p) {
     p.n_qtiles = (int)((nq + TILE_Q - 1) / TILE_Q);
     p.n_ctiles = (int)((h->ntotal + TILE_R - 1) / TILE_R);
-    p.xcd_split = 0;
     p.q32_tiles = 0;
+    p.share = k <= KP ? 1 : 0;
     const int rb64 = h->row_bytes / 64;
     const char* q32_env = getenv("FX_SCAN_Q32");
-    if (q32_env && atoi(q32_env) == 1 && nq <= 32 && h->row_bytes % 64 == 0 &&
+    if (q32_env && atoi(q32_env) == 1 && nq <= 32 && k <= KP && h->row_bytes % 64 == 0 &&
         (rb64 == 8 || rb64 == 12 || rb64 == 16 || rb64 == 24)) {
         // small batch (k_scan_q32): one 32-query tile; one round of one
         // workgroup per CU, each split >= 4 tiles; every corpus byte read once
         p.q32_tiles = (int)((nq + 31) / 32);
         p.qt_per_xcd = 0;
         p.splits = std::max(1, std::min(p.n_ctiles / 4, 256 / p.q32_tiles));
-        return;
-    }
-    const char* map_env = getenv("FX_SCAN_MAP");
-    if (map_env && atoi(map_env) == 1 && p.n_ctiles >= 8 * 4) {
-        // Corpus-partitioned placement (map_block): splits per XCD such that
-        // (a) each XCD runs >= 4 rounds of its 32 resident blocks, (b) a split
-        // is <= ~512 tiles, so the blocks streaming it side by side drift by
-        // less than the XCD's L2, (c) the last round is as full as possible,
-        // (d) every split keeps >= 4 tiles.  FX_SCAN_SPX overrides.
-        const int s_max = std::max(1, p.n_ctiles / 32);
-        int spx = getenv("FX_SCAN_SPX") ? atoi(getenv("FX_SCAN_SPX")) : 0;
-        if (spx <= 0) {
-            const int s_lo = std::min(s_max, std::max((128 + p.n_qtiles - 1) / p.n_qtiles,
-                                                      (p.n_ctiles + 8 * 512 - 1) / (8 * 512)));
-            spx = s_lo;
-            double best_eff = 0.0;
-            for (int s = s_lo; s <= std::min(s_max, 2 * s_lo); ++s) {
-                const double live = (double)p.n_qtiles * s;
-                const double eff = live / (std::ceil(live / 32.0) * 32.0);
-                if (eff > best_eff + 1e-9) { best_eff = eff; spx = s; }
-                if (eff > 0.985) break;
-            }
-        }
-        p.xcd_split = std::min(spx, s_max);
-        p.splits = 8 * p.xcd_split;
-        p.qt_per_xcd = 0;
         return;
     }
     p.qt_per_xcd = p.n_qtiles >= 8 ? (p.n_qtiles + 7) / 8 : 0;
@@ -216,15 +198,26 @@ void plan_scan(const FxIndex* h, int64_t nq, ScanParams& p) {
         if (eff > best_eff + 1e-9) { best_eff = eff; best = s; }
         if (eff > 0.985) break;
     }
+    if (k > KP) best = std::max(best, std::min(max_splits, (k + 3) / 4));
     p.splits = best;
 }
 
-// FX_F32_SPLIT=1 on an fp32 index: bring its F32S scan image up to date
+// k > KP: approx candidates the refine re-ranks exactly (k_refine_big)
+int big_k1(int k) { return k > KP ? std::max(2 * k, 64) : 0; }
+
+hipError_t ensure_pinned_count(FxIndex* h) {
+    if (h->pin_nf) return hipSuccess;
+    hipError_t e = hipHostMalloc((void**)&h->pin_nf, sizeof(int), hipHostMallocDefault);
+    if (e == hipSuccess) *h->pin_nf = 0;
+    return e;
+}
+
+// fp32 index (unless FX_F32_SPLIT=0): bring its F32S scan image up to date
 // (rows appended since the last search); *split says whether the scan uses it
 hipError_t update_scan_image(FxIndex* h, bool* split) {
     const int rb64 = h->row_bytes / 64;
     const char* split_env = getenv("FX_F32_SPLIT");
-    *split = split_env && atoi(split_env) == 1 && h->dtype == F32 && h->row_bytes % 64 == 0 &&
+    *split = !(split_env && atoi(split_env) == 0) && h->dtype == F32 && h->row_bytes % 64 == 0 &&
              (rb64 == 8 || rb64 == 12 || rb64 == 16 || rb64 == 24);
     if (!*split) return hipSuccess;
     hipStream_t s = h->stream();
@@ -257,17 +250,17 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
     HIP_TRY(h->qop.ensure((size_t)nq_pad * h->row_bytes));
     void* qop = h->qop.p;
     HIP_TRY(h->qeps.ensure((size_t)nq * 4));
-    // FX_F32_SPLIT=1: scan an fp32 index through its split-bf16 image (F32S:
+    // fp32 index: scan it through its split-bf16 image (F32S:
     // 3 bf16 products per term on the bf16 MFMA pipe instead of fp32 MFMA);
     // the refine and the certification still use the fp32 rows
     bool split = false;
     HIP_TRY(update_scan_image(h, &split));
     const int scan_dt = split ? (int)F32S : h->dtype;
     HIP_TRY(launch_prep_queries(qdev, q_dtype, nq, nq_pad, h->d, h->kdim, scan_dt, h->metric, (float*)h->qf32.p,
-                                qop, (float*)h->qeps.p, sqrt((double)h->max_sq), s));
+                                qop, (float*)h->qeps.p, h->max_sq_bits, s));
 
     ScanParams sp;
-    plan_scan(h, nq, sp);
+    plan_scan(h, nq, k, sp);
     sp.codes = split ? (const char*)h->split.p : h->codes;
     sp.norms = h->norms;
     sp.ntotal = h->ntotal;
@@ -341,6 +334,8 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
     rp.n_flag = n_flag;
     rp.flag_list = n_flag + 1;
     rp.prefetch = sp.q32_tiles > 0 ? 4 : 1;
+    rp.k1 = big_k1(k);
+    rp.force_fb = getenv("FX_FORCE_FALLBACK") ? atoi(getenv("FX_FORCE_FALLBACK")) : 0;
     HIP_TRY(launch_refine(h->dtype, h->metric, rp, s));
     if (h->profile) {
         HIP_TRY(hipEventRecord(e2, s));
@@ -348,13 +343,22 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
         h->ev_merge.emplace_back(e1, e2);
     }
 
-    // Certification result: uncertified queries are re-ranked by the exact
-    // fp64 scan (rare: only when the candidate margin is inside the scan's
-    // worst-case rounding bound).
-    int nf = 0;
-    HIP_TRY(hipMemcpyAsync(&nf, n_flag, 4, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    h->last_fallbacks = nf;
+    // Certification result: uncertified queries (rare: only when the
+    // candidate margin is inside the scan's worst-case rounding bound) are
+    // re-ranked by the exact fp64 scan.  Decided on the device: both
+    // fallback kernels are always enqueued and exit at once when the refine
+    // flagged nothing, so no host round trip sits inside the search.
+    if (sp.dbg == 0) {
+        const size_t nfb = (size_t)std::max<int64_t>(4096, nq) * k;
+        HIP_TRY(h->fbc_d.ensure(nfb * 4));
+        HIP_TRY(h->fbc_i.ensure(nfb * 4));
+        HIP_TRY(launch_exact_fallback(h->dtype, h->metric, h->codes, h->row_bytes, h->kdim, h->ntotal,
+                                      (const float*)h->qf32.p, n_flag, k, h->id_offset, (float*)h->fbc_d.p,
+                                      (int*)h->fbc_i.p, Dd, Id, s));
+    }
+    HIP_TRY(ensure_pinned_count(h));
+    HIP_TRY(hipMemcpyAsync(h->pin_nf, n_flag, 4, hipMemcpyDeviceToHost, s));
+    h->fb_pending = true;
     if (const char* cpath = getenv("FX_SCAN_CAND")) {  // diagnostics: raw scan candidate lists
         std::vector<float> cd(ncand);
         std::vector<int> ci(ncand);
@@ -382,23 +386,12 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
             fclose(f);
         }
     }
-    if (nf > 0 && sp.dbg == 0) {
-        const int fb_splits = (int)std::max<int64_t>(1, std::min<int64_t>(256, (h->ntotal + 4095) / 4096));
-        const int chunk = 64;
-        for (int f0 = 0; f0 < nf; f0 += chunk) {
-            const int nl = std::min(chunk, nf - f0);
-            const size_t per = (size_t)nl * fb_splits * 4 * KP;
-            HIP_TRY(h->fbc_d.ensure(per * 4));
-            HIP_TRY(h->fbc_i.ensure(per * 4));
-            HIP_TRY(launch_exact_fallback(h->dtype, h->metric, h->codes, h->row_bytes, h->kdim, h->ntotal,
-                                          (const float*)h->qf32.p, n_flag + 1 + f0, nl, k, h->id_offset,
-                                          (float*)h->fbc_d.p, (int*)h->fbc_i.p, fb_splits, Dd, Id, s));
-        }
-    }
     if (out_mem == FX_MEM_HOST) {
         HIP_TRY(hipMemcpyAsync(D, Dd, (size_t)nq * k * 4, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipMemcpyAsync(I, Id, (size_t)nq * k * 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
+        h->last_fallbacks = *h->pin_nf;
+        h->fb_pending = false;
     }
     return FX_OK;
 }
@@ -407,16 +400,17 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
 // while all of them are unchanged
 std::vector<uint64_t> graph_key(const FxIndex* h, int64_t nq, int q_dtype, int k) {
     ScanParams sp;
-    plan_scan(h, nq, sp);
-    const char* se = getenv("FX_F32_SPLIT");
+    plan_scan(h, nq, k, sp);
+    const char* se = getenv("FX_F32_SPLIT");  // (part of the key: unset and "1" both mean on)
     return {(uint64_t)nq, (uint64_t)q_dtype, (uint64_t)k, (uint64_t)h->ntotal, (uint64_t)h->id_offset,
-            (uint64_t)__builtin_bit_cast(uint32_t, h->max_sq), (uint64_t)(se ? atoi(se) : 0),
-            (uint64_t)sp.splits, (uint64_t)sp.q32_tiles, (uint64_t)sp.xcd_split, (uint64_t)sp.qt_per_xcd,
+            (uint64_t)(se ? atoi(se) : 1),
+            (uint64_t)(getenv("FX_FORCE_FALLBACK") ? atoi(getenv("FX_FORCE_FALLBACK")) : 0),
+            (uint64_t)sp.splits, (uint64_t)sp.q32_tiles, (uint64_t)sp.qt_per_xcd,
             (uint64_t)(uintptr_t)h->codes, (uint64_t)(uintptr_t)h->norms, (uint64_t)(uintptr_t)h->split.p,
             (uint64_t)(uintptr_t)h->qin.p, (uint64_t)(uintptr_t)h->qf32.p, (uint64_t)(uintptr_t)h->qop.p,
             (uint64_t)(uintptr_t)h->qeps.p, (uint64_t)(uintptr_t)h->gtau.p, (uint64_t)(uintptr_t)h->cand_d.p,
             (uint64_t)(uintptr_t)h->cand_i.p, (uint64_t)(uintptr_t)h->dws.p, (uint64_t)(uintptr_t)h->iws.p,
-            (uint64_t)(uintptr_t)h->flag.p};
+            (uint64_t)(uintptr_t)h->flag.p, (uint64_t)(uintptr_t)h->fbc_d.p, (uint64_t)(uintptr_t)h->fbc_i.p};
 }
 
 void graph_release(FxIndex* h) {
@@ -455,7 +449,7 @@ hipError_t graph_build(FxIndex* h, int64_t nq, int q_dtype, int k, bool split) {
     const int scan_dt = split ? (int)F32S : h->dtype;
     const int64_t nq_pad = round_up(nq, TILE_Q);
     ScanParams sp;
-    plan_scan(h, nq, sp);
+    plan_scan(h, nq, k, sp);
     sp.codes = split ? (const char*)h->split.p : h->codes;
     sp.norms = h->norms;
     sp.ntotal = h->ntotal;
@@ -486,18 +480,24 @@ hipError_t graph_build(FxIndex* h, int64_t nq, int q_dtype, int k, bool split) {
     rp.n_flag = n_flag;
     rp.flag_list = n_flag + 1;
     rp.prefetch = sp.q32_tiles > 0 ? 4 : 1;
+    rp.k1 = big_k1(k);
+    rp.force_fb = getenv("FX_FORCE_FALLBACK") ? atoi(getenv("FX_FORCE_FALLBACK")) : 0;
 
     if ((e = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal)) != hipSuccess) return e;
     g_graph_capture = true;
     hipError_t ce = hipMemcpyAsync(h->qin.p, h->ghq, qb, hipMemcpyHostToDevice, s);
     if (ce == hipSuccess)
         ce = launch_prep_queries(h->qin.p, q_dtype, nq, nq_pad, h->d, h->kdim, scan_dt, h->metric, (float*)h->qf32.p,
-                                 h->qop.p, (float*)h->qeps.p, sqrt((double)h->max_sq), s);
+                                 h->qop.p, (float*)h->qeps.p, h->max_sq_bits, s);
     if (ce == hipSuccess)
         ce = hipMemsetD32Async((hipDeviceptr_t)sp.gtau, 0xff800000u, (size_t)sp.n_qtiles * TILE_Q, s);
     if (ce == hipSuccess) ce = launch_scan(scan_dt, h->metric, sp, s);
     if (ce == hipSuccess) ce = hipMemsetAsync(n_flag, 0, 4, s);
     if (ce == hipSuccess) ce = launch_refine(h->dtype, h->metric, rp, s);
+    if (ce == hipSuccess)
+        ce = launch_exact_fallback(h->dtype, h->metric, h->codes, h->row_bytes, h->kdim, h->ntotal,
+                                   (const float*)h->qf32.p, n_flag, k, h->id_offset, (float*)h->fbc_d.p,
+                                   (int*)h->fbc_i.p, rp.D, rp.I, s);
     if (ce == hipSuccess) ce = hipMemcpyAsync(h->ghD, rp.D, nd * 4, hipMemcpyDeviceToHost, s);
     if (ce == hipSuccess) ce = hipMemcpyAsync(h->ghI, rp.I, nd * 8, hipMemcpyDeviceToHost, s);
     if (ce == hipSuccess) ce = hipMemcpyAsync(h->ghnf, n_flag, 4, hipMemcpyDeviceToHost, s);
@@ -516,9 +516,9 @@ hipError_t graph_build(FxIndex* h, int64_t nq, int q_dtype, int k, bool split) {
     return hipSuccess;
 }
 
-// Small host batches under FX_SEARCH_GRAPH=1: replay the captured search;
-// on a shape / buffer change run do_search and re-capture.  An uncertified
-// query (rare) re-runs do_search, which owns the exact fallback.
+// Small host batches under FX_SEARCH_GRAPH=1: replay the captured search
+// (the exact fallback included: it is device-gated); on a shape / buffer
+// change run do_search and re-capture.
 int graph_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int k, float* D, int64_t* I) {
     bool split = false;
     HIP_TRY(update_scan_image(h, &split));
@@ -527,13 +527,11 @@ int graph_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int k, floa
         memcpy(h->ghq, q, (size_t)nq * h->d * dtype_size(q_dtype));
         HIP_TRY(hipGraphLaunch(h->gexec, s));
         HIP_TRY(hipStreamSynchronize(s));
-        if (*h->ghnf == 0) {
-            memcpy(D, h->ghD, (size_t)nq * k * 4);
-            memcpy(I, h->ghI, (size_t)nq * k * 8);
-            h->last_fallbacks = 0;
-            return FX_OK;
-        }
-        return do_search(h, nq, q, q_dtype, FX_MEM_HOST, k, D, I, FX_MEM_HOST);
+        memcpy(D, h->ghD, (size_t)nq * k * 4);
+        memcpy(I, h->ghI, (size_t)nq * k * 8);
+        h->last_fallbacks = *h->ghnf;
+        h->fb_pending = false;
+        return FX_OK;
     }
     const int rc = do_search(h, nq, q, q_dtype, FX_MEM_HOST, k, D, I, FX_MEM_HOST);
     if (rc == FX_OK && !h->gfailed) {
@@ -616,6 +614,7 @@ void fx_index_free(FxIndex* h) {
         if (h->ghD) (void)hipHostFree(h->ghD);
         if (h->ghI) (void)hipHostFree(h->ghI);
         if (h->ghnf) (void)hipHostFree(h->ghnf);
+        if (h->pin_nf) (void)hipHostFree(h->pin_nf);
         for (auto& pr : h->ev_scan) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
         for (auto& pr : h->ev_merge) (void)hipEventDestroy(pr.second);
         if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
@@ -702,10 +701,6 @@ int fx_index_add(FxIndex* h, int64_t n, const void* x, int x_dtype, int x_mem) {
             HIP_TRY(hipStreamSynchronize(s));  // staging buffer reuse
         }
     }
-    unsigned bits = 0;
-    HIP_TRY(hipMemcpyAsync(&bits, h->max_sq_bits, 4, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    memcpy(&h->max_sq, &bits, 4);
     h->ntotal += n;
     return FX_OK;
 }
@@ -716,6 +711,7 @@ int fx_index_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_me
     if (nq < 0) return set_err(FX_E_ARG, "negative nq");
     if (k <= 0) return set_err(FX_E_ARG, "k must be positive (got %d)", k);
     if (k > FX_MAX_K) return set_err(FX_E_UNSUPPORTED, "k=%d exceeds FX_MAX_K=%d", k, FX_MAX_K);
+    static_assert(FX_MAX_K == FX_BIG_K, "ABI k limit = the big-k refine's");
     if (!check_dtype(q_dtype)) return set_err(FX_E_ARG, "bad query dtype %d", q_dtype);
     if (nq == 0) return FX_OK;
     if (!q || !D || !I) return set_err(FX_E_ARG, "null buffer");
@@ -723,17 +719,18 @@ int fx_index_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_me
     DeviceGuard g(h->device);
     if (h->ntotal == 0) {
         // faiss: empty index -> every slot missing (I = -1, D = FLT_MAX)
-        std::vector<float> dv((size_t)nq * k, h->metric == L2 ? FLT_MAX : -FLT_MAX);
-        std::vector<int64_t> iv((size_t)nq * k, -1);
+        const float dfill = h->metric == L2 ? FLT_MAX : -FLT_MAX;
         if (out_mem == FX_MEM_HOST) {
-            memcpy(D, dv.data(), dv.size() * 4);
-            memcpy(I, iv.data(), iv.size() * 8);
-        } else {
-            HIP_TRY(hipMemcpyAsync(D, dv.data(), dv.size() * 4, hipMemcpyHostToDevice, h->stream()));
-            HIP_TRY(hipMemcpyAsync(I, iv.data(), iv.size() * 8, hipMemcpyHostToDevice, h->stream()));
-            HIP_TRY(hipStreamSynchronize(h->stream()));
+            std::fill(D, D + (size_t)nq * k, dfill);
+            std::fill(I, I + (size_t)nq * k, (int64_t)-1);
+        } else {  // stream-ordered fills: -1 is all ones in two's complement
+            uint32_t bits;
+            memcpy(&bits, &dfill, 4);
+            HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)D, bits, (size_t)nq * k, h->stream()));
+            HIP_TRY(hipMemsetAsync(I, 0xff, (size_t)nq * k * 8, h->stream()));
         }
         h->last_fallbacks = 0;
+        h->fb_pending = false;
         return FX_OK;
     }
     const char* ge = getenv("FX_SEARCH_GRAPH");
@@ -745,6 +742,13 @@ int fx_index_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_me
 
 int fx_index_last_fallbacks(FxIndex* h, int64_t* out) {
     if (!h || !out) return set_err(FX_E_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (h->fb_pending) {  // a device-resident search left its count in flight
+        DeviceGuard g(h->device);
+        HIP_TRY(hipStreamSynchronize(h->stream()));
+        h->last_fallbacks = *h->pin_nf;
+        h->fb_pending = false;
+    }
     *out = h->last_fallbacks;
     return FX_OK;
 }
@@ -759,7 +763,6 @@ int fx_index_reset(FxIndex* h) {
         HIP_TRY(hipMemset(h->codes, 0, (size_t)h->cap_rows * h->row_bytes));
         HIP_TRY(hipMemsetD32((hipDeviceptr_t)h->norms, 0x7f800000u, (size_t)h->cap_rows));
     }
-    h->max_sq = 0.0f;
     h->ntotal = 0;
     h->split_rows = 0;
     return FX_OK;
@@ -864,7 +867,7 @@ int fx_index_read(const char* path, int storage_dtype, int device, FxIndex** out
 
 int fx_merge_shards(int metric, int nshards, int64_t nq, int k, const float* D_in, const int64_t* I_in, float* D_out,
                     int64_t* I_out, int device, void* stream) {
-    if (nshards <= 0 || nq < 0 || k <= 0 || k > 64) return set_err(FX_E_ARG, "bad merge shape");
+    if (nshards <= 0 || nq < 0 || k <= 0 || k > FX_MAX_K) return set_err(FX_E_ARG, "bad merge shape");
     if (!D_in || !I_in || !D_out || !I_out) return set_err(FX_E_ARG, "null buffer");
     if (metric != FX_METRIC_L2 && metric != FX_METRIC_INNER_PRODUCT) return set_err(FX_E_ARG, "bad metric");
     DeviceGuard g(device);

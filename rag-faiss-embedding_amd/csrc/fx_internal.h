@@ -11,6 +11,7 @@ constexpr int TILE_R = 128;   // corpus rows per tile (MFMA M side)
 constexpr int TILE_Q = 128;   // queries per tile      (MFMA N side)
 constexpr int STAGE_B = 128;  // bytes of each row's K staged per pipeline stage
 constexpr int KP = 32;        // candidates kept per (query, corpus split)
+constexpr int FX_BIG_K = 1024;  // largest k (k > KP: k_refine_big; == FX_MAX_K of the ABI)
 constexpr int CAP = 64;       // LDS candidate-list capacity per query (2*KP)
 constexpr int ROW_ALIGN = 128;  // row stride alignment in bytes (== STAGE_B)
 constexpr int SCAN_THREADS = 256;
@@ -55,11 +56,10 @@ struct ScanParams {
     unsigned long long* trace;  // diagnostics only (FX_SCAN_TRACE): per block
                                 // {xcc | hw_id << 8 | qtile << 32, split, t_start, t_end}
     unsigned* dbgbuf;           // diagnostics only (FX_SCAN_DBG & 32): operand self-check
-    int xcd_split;              // > 0: corpus-partitioned placement (FX_SCAN_MAP=1): XCD x owns
-                                // splits [x*xcd_split, (x+1)*xcd_split) of every query tile;
-                                // then splits == 8*xcd_split and qt_per_xcd == 0
     int q32_tiles;              // > 0: small-batch scan k_scan_q32 (FX_SCAN_Q32=1) over this many
                                 // 32-query tiles (one workgroup per tile and split)
+    int share;                  // 1: splits publish their KP-th key to gtau and prune with it
+                                // (k <= KP); 0: no cross-split pruning (k > KP, k_refine_big)
 };
 
 struct RefineParams {
@@ -79,7 +79,21 @@ struct RefineParams {
     int* n_flag;           // uncertified counter
     int* flag_list;        // [nq] uncertified query ids
     int prefetch;          // > 1: phase-1 loads issued 4 chunks at a time (small-batch scan)
+    int k1;                // k > KP: approx candidates re-ranked exactly (2k, <= 2 FX_BIG_K)
+    int force_fb;          // test hook (FX_FORCE_FALLBACK=1): flag every query -> exact fallback
 };
+
+// exact fallback (k_fb_scan / k_fb_merge): corpus splits per flagged query,
+// decided on the device from the flagged count nf; items nf * fbs <=
+// max(4096, nf), so the candidate buffer is max(4096, nq) * k entries
+constexpr int FB_SCAN_GRID = 1024, FB_MERGE_GRID = 256;
+__host__ __device__ inline int fb_splits_for(int nf, int64_t ntotal) {
+    int s = nf >= 4096 ? 1 : 4096 / (nf > 0 ? nf : 1);
+    if (s > 256) s = 256;
+    const int64_t by_rows = ntotal / 1024 > 0 ? ntotal / 1024 : 1;
+    if (s > by_rows) s = (int)by_rows;
+    return s < 1 ? 1 : s;
+}
 
 // True on a thread that is capturing a search into a hipGraph (fx_index.cpp
 // graph_build): the scan launchers then skip hipFuncSetAttribute, which the
@@ -92,19 +106,19 @@ hipError_t launch_convert_rows(const void* x, int x_dt, int64_t n, int d, void* 
                                hipStream_t s);
 hipError_t launch_prep_queries(const void* q, int q_dt, int64_t nq, int64_t nq_pad, int d, int kdim,
                                int st_dt, int metric, float* qf32, void* qop, float* qeps,
-                               double max_norm, hipStream_t s);
+                               const unsigned* max_sq_bits, hipStream_t s);
 hipError_t launch_scan(int st_dt, int metric, const ScanParams& p, hipStream_t s);
 // fx_scan.hip: the MFMA scan; *handled = false when it has no kernel for p.row_bytes
 hipError_t launch_scan_mfma(int st_dt, int metric, const ScanParams& p, hipStream_t s, bool* handled);
-// fx_scan5.hip: the 8-wave K-split variant (FX_SCAN_V5=1; =2 with the staggered epilogue)
-hipError_t launch_scan_mfma5(int st_dt, int metric, const ScanParams& p, hipStream_t s, bool stag, bool* handled);
 // fx_scan_q32.hip: the small-batch scan (p.q32_tiles > 0)
 hipError_t launch_scan_q32(int st_dt, int metric, const ScanParams& p, hipStream_t s, bool* handled);
 hipError_t launch_refine(int st_dt, int metric, const RefineParams& p, hipStream_t s);
+// both fallback launches, always enqueued; they read the flagged count at
+// n_flag[0] (list at n_flag + 1) and do nothing when it is 0
 hipError_t launch_exact_fallback(int st_dt, int metric, const char* codes, int row_bytes, int kdim,
-                                 int64_t ntotal, const float* qf32, const int* qlist, int nlist,
-                                 int k, int64_t id_offset, float* cand_d, int* cand_i, int fb_splits,
-                                 float* D, int64_t* I, hipStream_t s);
+                                 int64_t ntotal, const float* qf32, const int* n_flag, int k,
+                                 int64_t id_offset, float* cand_d, int* cand_i, float* D, int64_t* I,
+                                 hipStream_t s);
 hipError_t launch_merge_shards(int metric, int nshards, int64_t nq, int k, const float* D_in,
                                const int64_t* I_in, float* D_out, int64_t* I_out, hipStream_t s);
 // fp32 code rows [r0, r1) -> their F32S scan image (same row stride)

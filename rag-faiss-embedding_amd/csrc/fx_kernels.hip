@@ -20,8 +20,11 @@
 //                    differences, one rounding to fp32 -- the oracle's
 //                    definition), order by (D, id), certify the top-k against
 //                    the scan's error bound.
-//   k_exact_scan /   fallback for uncertified queries: exact fp64 scan of every
-//   k_merge_exact    row, then (D, id) top-k.
+//   k_refine_big     the same for k > KP (block top-K in LDS, scan without
+//                    the shared threshold).
+//   k_fb_scan /      fallback for uncertified queries, gated on the device
+//   k_fb_merge       (exit at once when none): exact fp64 scan of every row,
+//                    then (D, id) top-k.
 //   k_merge_shards   multi-GPU: merge G gathered per-shard top-k lists.
 //   k_synth          counter-based synthetic corpus (oracle/flat_l2.c twin).
 #include "fx_device.h"
@@ -37,36 +40,100 @@ thread_local bool g_graph_capture = false;
 // ---------------------------------------------------------------------------
 // add(): convert rows into the code matrix, compute |y|^2
 // ---------------------------------------------------------------------------
+// One wave per row; each lane converts 16-B output chunks (4 fp32 or 8
+// bf16/fp16 values) read with 16-B / 8-B vector loads when the input rows
+// are 16-B aligned (`vec`), else element by element.  Elements past d are the
+// row's zero padding.  |y|^2 of the stored values in fp32; the largest |y|^2
+// (certification margin) is reduced per workgroup in LDS and published with
+// one global atomicMax per workgroup.
+__device__ __forceinline__ void load_chunk_in(const void* __restrict__ x, int x_dt, int64_t base, int e0, int d,
+                                              int E, bool vec, float* v) {
+    if (vec && e0 + E <= d) {
+        if (x_dt == F32) {
+            const float4* p4 = (const float4*)((const float*)x + base + e0);
+            const float4 a = p4[0];
+            v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+            if (E == 8) {
+                const float4 b = p4[1];
+                v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+            }
+        } else {
+            const uint16_t* p = (const uint16_t*)x + base + e0;
+            uint32_t w[4];
+            if (E == 8) {
+                const uint4 a = *(const uint4*)p;
+                w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+            } else {
+                const uint2 a = *(const uint2*)p;
+                w[0] = a.x; w[1] = a.y;
+            }
+            for (int j = 0; j < E; ++j) {
+                const uint16_t hv = (uint16_t)(w[j >> 1] >> (16 * (j & 1)));
+                v[j] = x_dt == BF16 ? bf2f(hv) : h2f(hv);
+            }
+        }
+        return;
+    }
+    for (int j = 0; j < E; ++j) v[j] = e0 + j < d ? load_elem(x, base + e0 + j, x_dt) : 0.0f;
+}
+
 __global__ __launch_bounds__(256) void k_convert_rows(const void* __restrict__ x, int x_dt, int64_t n, int d,
                                                       void* __restrict__ codes, int st_dt, int kdim,
                                                       float* __restrict__ norms, unsigned* __restrict__ max_sq_bits,
-                                                      int normalize) {
+                                                      int normalize, int vec) {
+    __shared__ unsigned bmax;
+    if (threadIdx.x == 0) bmax = 0u;
+    __syncthreads();
     const int lane = threadIdx.x & 63;
     const int64_t nwaves = (int64_t)gridDim.x * 4;
+    const int E = st_dt == F32 ? 4 : 8;  // values per 16-B output chunk
+    const int nchunk = kdim / E;         // kdim * esize = row_bytes, a multiple of 128
+    unsigned my_max = 0u;
     for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < n; r += nwaves) {
+        const int64_t base = r * d;
         float scale = 1.0f;
         if (normalize) {
             double s = 0.0;
-            for (int c = lane; c < d; c += 64) {
-                double v = load_elem(x, r * d + c, x_dt);
-                s += v * v;
+            for (int c = lane; c < nchunk; c += 64) {
+                float v[8];
+                load_chunk_in(x, x_dt, base, c * E, d, E, vec != 0, v);
+                for (int j = 0; j < E; ++j) s = fma((double)v[j], (double)v[j], s);
             }
             s = wave_sum_f64(s);
             scale = s > 0.0 ? (float)(1.0 / sqrt(s)) : 1.0f;
         }
         float sq = 0.0f;
-        for (int c = lane; c < kdim; c += 64) {
-            float v = c < d ? load_elem(x, r * d + c, x_dt) * scale : 0.0f;
-            float st = round_to(v, st_dt);
-            store_elem(codes, r * (int64_t)kdim + c, st_dt, st);
-            sq = fmaf(st, st, sq);
+        char* out = (char*)codes + r * (int64_t)kdim * (st_dt == F32 ? 4 : 2);
+        for (int c = lane; c < nchunk; c += 64) {
+            float v[8];
+            load_chunk_in(x, x_dt, base, c * E, d, E, vec != 0, v);
+            if (st_dt == F32) {
+                float4 o;
+                o.x = v[0] * scale; o.y = v[1] * scale; o.z = v[2] * scale; o.w = v[3] * scale;
+                sq = fmaf(o.x, o.x, sq); sq = fmaf(o.y, o.y, sq); sq = fmaf(o.z, o.z, sq); sq = fmaf(o.w, o.w, sq);
+                *(float4*)(out + c * 16) = o;
+            } else {
+                uint32_t w[4];
+                for (int j = 0; j < 8; j += 2) {
+                    const uint16_t h0 = st_dt == BF16 ? f2bf(v[j] * scale) : f2h(v[j] * scale);
+                    const uint16_t h1 = st_dt == BF16 ? f2bf(v[j + 1] * scale) : f2h(v[j + 1] * scale);
+                    const float s0 = st_dt == BF16 ? bf2f(h0) : h2f(h0), s1 = st_dt == BF16 ? bf2f(h1) : h2f(h1);
+                    sq = fmaf(s0, s0, sq);
+                    sq = fmaf(s1, s1, sq);
+                    w[j >> 1] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+                }
+                *(uint4*)(out + c * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+            }
         }
         sq = wave_sum_f32(sq);
         if (lane == 0) {
             norms[r] = sq;
-            atomicMax(max_sq_bits, __float_as_uint(sq));  // positive floats order as uints
+            my_max = max(my_max, __float_as_uint(sq));  // non-negative floats order as uints
         }
     }
+    if (lane == 0 && my_max) atomicMax(&bmax, my_max);
+    __syncthreads();
+    if (threadIdx.x == 0 && bmax) atomicMax(max_sq_bits, bmax);
 }
 
 // fp32 rows -> F32S scan image: row r = [rn_bf16(v) for v in row | rn_bf16(v - hi)]
@@ -97,7 +164,8 @@ __global__ __launch_bounds__(256) void k_split_rows(const float* __restrict__ co
 __global__ __launch_bounds__(256) void k_prep_queries(const void* __restrict__ q, int q_dt, int64_t nq,
                                                       int64_t nq_pad, int d, int kdim, int st_dt, int metric,
                                                       float* __restrict__ qf32, void* __restrict__ qop,
-                                                      float* __restrict__ qeps, double max_norm, double gamma) {
+                                                      float* __restrict__ qeps, const unsigned* __restrict__ max_sq_bits,
+                                                      double gamma) {
     const int lane = threadIdx.x & 63;
     const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= nq_pad) return;
@@ -133,7 +201,9 @@ __global__ __launch_bounds__(256) void k_prep_queries(const void* __restrict__ q
         // kdim terms (gamma = K u / (1 - K u)), one more rounding in the key
         // (u), and the query's rounding to the storage dtype (delta).
         const double u = 5.9604644775390625e-8;  // 2^-24
-        const double xn = sqrt(s), M = max_norm;
+        // M = the largest stored row norm, read on the device (add() never
+        // waits for the host to learn it)
+        const double xn = sqrt(s), M = sqrt((double)__uint_as_float(*max_sq_bits));
         // F32S: the split scan drops lo*lo and both residuals v - hi - lo;
         // per product <= 3 * 2^-16 (1 + 2^-7) |x_k||y_k|;
         // gamma then covers its 3 K products (launch_prep_queries)
@@ -513,7 +583,114 @@ __global__ __launch_bounds__(256) void k_refine(RefineParams p) {
         const float kth = __shfl(key, p.k - 1, 64);
         const double bound = (METRIC == L2 ? (double)td + xn2 : (double)td) - (double)p.qeps[q];
         const double kup = (double)kth + fabs((double)kth) * 2.384185791015625e-7;  // + 2 ulp
-        if (!(kup < bound) && lane == 0) {
+        if (!(kup < bound) && lane == 0 && !p.force_fb) {
+            const int pos = atomicAdd(p.n_flag, 1);
+            p.flag_list[pos] = (int)q;
+        }
+    }
+    if (p.force_fb && lane == 0) {
+        const int pos = atomicAdd(p.n_flag, 1);
+        p.flag_list[pos] = (int)q;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k > KP: refine without the fixed 64-lane lists (one workgroup per query)
+// ---------------------------------------------------------------------------
+// The scan ran with share = 0 (no cross-split threshold), so a split drops a
+// row only when its own list is full, and then every dropped row has approx
+// key >= that split's KP-th output entry.  Phase 1 selects the K1 best approx
+// keys over all splits (block top-K in LDS) and the bound tb below which no
+// unselected row can lie: min(KP-th entry of every full split, K1-th kept
+// entry when candidates were cut).  Phase 2 computes the selected rows'
+// exact distances (fp64, one rounding), phase 3 orders them by (D, id),
+// writes the top-k and certifies it against tb like k_refine.
+template <int DT, int METRIC>
+__global__ __launch_bounds__(BT_THREADS) void k_refine_big(RefineParams p) {
+    __shared__ float sd[BT_MAXB];
+    __shared__ int si[BT_MAXB];
+    __shared__ float ed[BT_MAXB];
+    __shared__ int ei[BT_MAXB];
+    __shared__ BtState<int> st;
+    __shared__ unsigned t_split;
+    __shared__ double red[BT_THREADS / 64];
+    const int64_t q = blockIdx.x;
+    if (q >= p.nq) return;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int qtile = (int)(q / TILE_Q), qq = (int)(q % TILE_Q);
+    const int K1 = p.k1, B = bt_cap(K1);
+    if (tid == 0) t_split = f2ord(FX_INF);
+    bt_init(&st);
+    const int ncand = p.splits * KP;
+    for (int c0 = 0; c0 < ncand; c0 += BT_THREADS) {
+        const int c = c0 + tid;
+        float d = FX_INF;
+        int i = INT_MAX;
+        bool valid = false;
+        if (c < ncand) {
+            const int s = c / KP, j = c - s * KP;
+            const int64_t off = (((int64_t)qtile * p.splits + s) * TILE_Q + qq) * KP + j;
+            const int ii = p.cand_i[off];
+            if (ii >= 0) {
+                d = p.cand_d[off];
+                i = ii;
+                valid = true;
+                if (j == KP - 1) atomicMin(&t_split, f2ord(d));  // a full split's KP-th key
+            }
+        }
+        bt_round(sd, si, &st, K1, B, d, i, valid);
+    }
+    bt_flush(sd, si, &st, K1, B);
+    const int n1 = st.cnt;
+    float tb = ord2f(t_split);
+    if (st.total > n1) tb = fminf(tb, sd[n1 - 1]);
+
+    // phase 2: exact keys of the n1 selected rows, 16 lanes per row
+    const float* xq = p.qf32 + q * (int64_t)p.kdim;
+    const int grp = tid >> 4, sub = tid & 15;
+    for (int r0 = 0; r0 < n1; r0 += BT_THREADS / 16) {
+        const int r = r0 + grp;
+        double a = 0.0;
+        if (r < n1) a = exact_partial<DT, METRIC>(xq, p.codes + (int64_t)si[r] * p.row_bytes, p.row_bytes, sub, 16);
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+        if (sub == 0 && r < n1) {
+            ed[r] = METRIC == L2 ? (float)a : -(float)a;
+            ei[r] = si[r];
+        }
+    }
+    int n2 = 2;
+    while (n2 < n1) n2 <<= 1;
+    for (int t = n1 + tid; t < n2; t += BT_THREADS) {
+        ed[t] = FX_INF;
+        ei[t] = INT_MAX;
+    }
+    double xn2 = 0.0;
+    if (METRIC == L2) {
+        for (int c = tid; c < p.kdim; c += BT_THREADS) xn2 = fma((double)xq[c], (double)xq[c], xn2);
+        xn2 = wave_sum_f64(xn2);
+        if (lane == 0) red[tid >> 6] = xn2;
+    }
+    bt_sort(ed, ei, n2);  // (syncs: ed/ei and red complete)
+    if (METRIC == L2) xn2 = red[0] + red[1] + red[2] + red[3];
+
+    // phase 3: top-k out (faiss padding past the candidates), certification
+    for (int t = tid; t < p.k; t += BT_THREADS) {
+        const bool valid = t < n1;
+        p.D[q * p.k + t] = valid ? (METRIC == L2 ? ed[t] : -ed[t]) : (METRIC == L2 ? FLT_MAX : -FLT_MAX);
+        p.I[q * p.k + t] = valid ? (int64_t)ei[t] + p.id_offset : (int64_t)-1;
+    }
+    if (tid == 0) {
+        bool ok;
+        if (!(tb < FX_INF)) ok = true;  // no row was dropped anywhere: the candidates are every row
+        else if (n1 < p.k) ok = false;
+        else {
+            const float kth = ed[p.k - 1];
+            const double bound = (METRIC == L2 ? (double)tb + xn2 : (double)tb) - (double)p.qeps[q];
+            const double kup = (double)kth + fabs((double)kth) * 2.384185791015625e-7;  // + 2 ulp
+            ok = kup < bound;
+        }
+        if (!ok || p.force_fb) {
             const int pos = atomicAdd(p.n_flag, 1);
             p.flag_list[pos] = (int)q;
         }
@@ -521,74 +698,82 @@ __global__ __launch_bounds__(256) void k_refine(RefineParams p) {
 }
 
 // ---------------------------------------------------------------------------
-// exact fallback: every row's exact key, (key, id) top-KP per wave
+// exact fallback for uncertified queries, decided on the device: the host
+// always enqueues these two launches after the refine; they read the
+// uncertified count n_flag[0] (list at n_flag + 1) and exit at once when it
+// is 0, so a device-resident search never waits for the host.
+// k_fb_scan: work item = (flagged query f, corpus split); exact fp64 key of
+// every row of the split, block top-k -> cd/ci[item][k].
+// k_fb_merge: per flagged query, top-k of its splits' lists -> D / I.
 // ---------------------------------------------------------------------------
 template <int DT, int METRIC>
-__global__ __launch_bounds__(256) void k_exact_scan(const char* __restrict__ codes, int row_bytes, int kdim,
-                                                    int64_t ntotal, const float* __restrict__ qf32,
-                                                    const int* __restrict__ qlist, int fb_splits,
-                                                    float* __restrict__ cand_d, int* __restrict__ cand_i) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int f = blockIdx.x / fb_splits, split = blockIdx.x % fb_splits;
-    const int64_t q = qlist[f];
-    const float* xq = qf32 + q * (int64_t)kdim;
-    const int64_t r0 = ntotal * split / fb_splits, r1 = ntotal * (split + 1) / fb_splits;
-    float bd = FX_INF, td = FX_INF;
-    int bi = INT_MAX, ti = INT_MAX;
-    for (int64_t base = r0 + (int64_t)wave * 64; base < r1; base += 256) {
-        const int64_t row = base + lane;
-        float key = FX_INF;
-        int id = INT_MAX;
-        if (row < r1) {
-            const double v = exact_partial<DT, METRIC>(xq, codes + row * row_bytes, row_bytes, 0, 1);
-            key = METRIC == L2 ? (float)v : -(float)v;
-            id = (int)row;
+__global__ __launch_bounds__(BT_THREADS) void k_fb_scan(const char* __restrict__ codes, int row_bytes, int kdim,
+                                                        int64_t ntotal, const float* __restrict__ qf32,
+                                                        const int* __restrict__ n_flag, int k,
+                                                        float* __restrict__ cd, int* __restrict__ ci) {
+    __shared__ float sd[BT_MAXB];
+    __shared__ int si[BT_MAXB];
+    __shared__ BtState<int> st;
+    const int nf = n_flag[0];
+    if (nf <= 0) return;
+    const int* qlist = n_flag + 1;
+    const int fbs = fb_splits_for(nf, ntotal), B = bt_cap(k);
+    const int64_t items = (int64_t)nf * fbs;
+    for (int64_t w = blockIdx.x; w < items; w += gridDim.x) {
+        const int f = (int)(w / fbs), split = (int)(w % fbs);
+        const float* xq = qf32 + (int64_t)qlist[f] * kdim;
+        const int64_t r0 = ntotal * split / fbs, r1 = ntotal * (split + 1) / fbs;
+        bt_init(&st);
+        for (int64_t base = r0; base < r1; base += BT_THREADS) {
+            const int64_t row = base + threadIdx.x;
+            const bool valid = row < r1;
+            float key = FX_INF;
+            if (valid) {
+                const double v = exact_partial<DT, METRIC>(xq, codes + row * row_bytes, row_bytes, 0, 1);
+                key = METRIC == L2 ? (float)v : -(float)v;
+            }
+            bt_round(sd, si, &st, k, B, key, valid ? (int)row : INT_MAX, valid);
         }
-        const bool pass = id != INT_MAX && key_lt(key, id, td, ti);
-        if (!__any(pass)) continue;
-        if (!pass) { key = FX_INF; id = INT_MAX; }
-        sort64(key, id, lane);
-        merge_into(bd, bi, key, id, lane);
-        td = __shfl(bd, KP - 1, 64);
-        ti = __shfl(bi, KP - 1, 64);
-    }
-    if (lane < KP) {
-        const int64_t o = (((int64_t)f * fb_splits + split) * 4 + wave) * KP + lane;
-        cand_d[o] = bd;
-        cand_i[o] = bi == INT_MAX ? -1 : bi;
+        bt_flush(sd, si, &st, k, B);
+        const int c = st.cnt;
+        for (int t = threadIdx.x; t < k; t += BT_THREADS) {
+            cd[w * k + t] = t < c ? sd[t] : FX_INF;
+            ci[w * k + t] = t < c ? si[t] : -1;
+        }
+        __syncthreads();
     }
 }
 
 template <int METRIC>
-__global__ __launch_bounds__(256) void k_merge_exact(const float* __restrict__ cand_d, const int* __restrict__ cand_i,
-                                                     int per_query, const int* __restrict__ qlist, int nlist, int k,
-                                                     int64_t id_offset, float* __restrict__ D, int64_t* __restrict__ I) {
-    const int lane = threadIdx.x & 63;
-    const int f = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (f >= nlist) return;
-    float bd = FX_INF, td = FX_INF;
-    int bi = INT_MAX, ti = INT_MAX;
-    for (int base = 0; base < per_query; base += 64) {
-        const int c = base + lane;
-        float d = FX_INF;
-        int i = INT_MAX;
-        if (c < per_query) {
-            const int ii = cand_i[(int64_t)f * per_query + c];
-            if (ii >= 0) { d = cand_d[(int64_t)f * per_query + c]; i = ii; }
+__global__ __launch_bounds__(BT_THREADS) void k_fb_merge(const int* __restrict__ n_flag, int64_t ntotal, int k,
+                                                         const float* __restrict__ cd, const int* __restrict__ ci,
+                                                         int64_t id_offset, float* __restrict__ D,
+                                                         int64_t* __restrict__ I) {
+    __shared__ float sd[BT_MAXB];
+    __shared__ int si[BT_MAXB];
+    __shared__ BtState<int> st;
+    const int nf = n_flag[0];
+    if (nf <= 0) return;
+    const int* qlist = n_flag + 1;
+    const int fbs = fb_splits_for(nf, ntotal), B = bt_cap(k);
+    const int64_t per = (int64_t)fbs * k;
+    for (int f = blockIdx.x; f < nf; f += gridDim.x) {
+        bt_init(&st);
+        for (int64_t c0 = 0; c0 < per; c0 += BT_THREADS) {
+            const int64_t c = (int64_t)f * per + c0 + threadIdx.x;
+            const bool in = c0 + threadIdx.x < per;
+            const int ii = in ? ci[c] : -1;
+            bt_round(sd, si, &st, k, B, ii >= 0 ? cd[c] : FX_INF, ii >= 0 ? ii : INT_MAX, ii >= 0);
         }
-        const bool pass = i != INT_MAX && key_lt(d, i, td, ti);
-        if (!__any(pass)) continue;
-        if (!pass) { d = FX_INF; i = INT_MAX; }
-        sort64(d, i, lane);
-        merge_into(bd, bi, d, i, lane);
-        td = __shfl(bd, KP - 1, 64);
-        ti = __shfl(bi, KP - 1, 64);
-    }
-    const int64_t q = qlist[f];
-    if (lane < k) {
-        const bool valid = bi != INT_MAX;
-        D[q * k + lane] = valid ? (METRIC == L2 ? bd : -bd) : (METRIC == L2 ? FLT_MAX : -FLT_MAX);
-        I[q * k + lane] = valid ? (int64_t)bi + id_offset : (int64_t)-1;
+        bt_flush(sd, si, &st, k, B);
+        const int64_t q = qlist[f];
+        const int c = st.cnt;
+        for (int t = threadIdx.x; t < k; t += BT_THREADS) {
+            const bool valid = t < c;
+            D[q * k + t] = valid ? (METRIC == L2 ? sd[t] : -sd[t]) : (METRIC == L2 ? FLT_MAX : -FLT_MAX);
+            I[q * k + t] = valid ? (int64_t)si[t] + id_offset : (int64_t)-1;
+        }
+        __syncthreads();
     }
 }
 
@@ -631,6 +816,41 @@ __global__ __launch_bounds__(256) void k_merge_shards(int nshards, int64_t nq, i
     }
 }
 
+// k > 64: one workgroup per query, block top-k over the G*k gathered entries
+template <int METRIC>
+__global__ __launch_bounds__(BT_THREADS) void k_merge_shards_big(int nshards, int64_t nq, int k,
+                                                                 const float* __restrict__ Din,
+                                                                 const int64_t* __restrict__ Iin,
+                                                                 float* __restrict__ Dout,
+                                                                 int64_t* __restrict__ Iout) {
+    __shared__ float sd[BT_MAXB];
+    __shared__ long long si[BT_MAXB];
+    __shared__ BtState<long long> st;
+    const int64_t q = blockIdx.x;
+    if (q >= nq) return;
+    const int B = bt_cap(k), total = nshards * k;
+    bt_init(&st);
+    for (int c0 = 0; c0 < total; c0 += BT_THREADS) {
+        const int c = c0 + threadIdx.x;
+        long long ii = -1;
+        float d = FX_INF;
+        if (c < total) {
+            const int sh = c / k, j = c - sh * k;
+            const int64_t off = ((int64_t)sh * nq + q) * k + j;
+            ii = Iin[off];
+            if (ii >= 0) d = METRIC == L2 ? Din[off] : -Din[off];
+        }
+        bt_round(sd, si, &st, k, B, d, ii >= 0 ? ii : LLONG_MAX, ii >= 0);
+    }
+    bt_flush(sd, si, &st, k, B);
+    const int c = st.cnt;
+    for (int t = threadIdx.x; t < k; t += BT_THREADS) {
+        const bool valid = t < c;
+        Dout[q * k + t] = valid ? (METRIC == L2 ? sd[t] : -sd[t]) : (METRIC == L2 ? FLT_MAX : -FLT_MAX);
+        Iout[q * k + t] = valid ? (int64_t)si[t] : (int64_t)-1;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // synthetic corpus and fp32 read-back
 // ---------------------------------------------------------------------------
@@ -670,8 +890,9 @@ static inline int grid_for(int64_t items, int per_block, int cap) {
 hipError_t launch_convert_rows(const void* x, int x_dt, int64_t n, int d, void* codes_row0, int st_dt, int kdim,
                                float* norms_row0, unsigned* max_sq_bits, int normalize, hipStream_t s) {
     if (n <= 0) return hipSuccess;
+    const int vec = ((int64_t)d * (x_dt == F32 ? 4 : 2)) % 16 == 0 && ((uintptr_t)x & 15) == 0;
     hipLaunchKernelGGL(k_convert_rows, dim3(grid_for(n, 4, 65536)), dim3(256), 0, s, x, x_dt, n, d, codes_row0,
-                       st_dt, kdim, norms_row0, max_sq_bits, normalize);
+                       st_dt, kdim, norms_row0, max_sq_bits, normalize, vec);
     return hipGetLastError();
 }
 
@@ -683,13 +904,14 @@ hipError_t launch_split_rows(const float* codes, int kdim, int64_t r0, int64_t r
 }
 
 hipError_t launch_prep_queries(const void* q, int q_dt, int64_t nq, int64_t nq_pad, int d, int kdim, int st_dt,
-                               int metric, float* qf32, void* qop, float* qeps, double max_norm, hipStream_t s) {
+                               int metric, float* qf32, void* qop, float* qeps, const unsigned* max_sq_bits,
+                               hipStream_t s) {
     const double u = 5.9604644775390625e-8;
     // terms accumulated by the scan's fp32 MFMA chain: K products (3 K for F32S) + srcC
     const double nt = st_dt == F32S ? 3.0 * kdim + 1.0 : (double)kdim;
     const double gamma = nt * u / (1.0 - nt * u);
     hipLaunchKernelGGL(k_prep_queries, dim3((unsigned)((nq_pad + 3) / 4)), dim3(256), 0, s, q, q_dt, nq, nq_pad, d,
-                       kdim, st_dt, metric, qf32, qop, qeps, max_norm, gamma);
+                       kdim, st_dt, metric, qf32, qop, qeps, max_sq_bits, gamma);
     return hipGetLastError();
 }
 
@@ -713,21 +935,13 @@ hipError_t launch_scan(int st_dt, int metric, const ScanParams& p, hipStream_t s
         return handled ? e : hipErrorInvalidValue;
     }
     if (st_dt == F32S) {  // the split-fp32 operand exists only for the MFMA scans
-        static const int v5s = getenv("FX_SCAN_V5") != nullptr ? atoi(getenv("FX_SCAN_V5")) : 0;
         bool handled = false;
-        if (v5s) {
-            hipError_t e = launch_scan_mfma5(st_dt, metric, p, s, v5s == 2, &handled);
-            if (handled) return e;
-        }
         hipError_t e = launch_scan_mfma(st_dt, metric, p, s, &handled);
         return handled ? e : hipErrorInvalidValue;
     }
     if (!getenv("FX_SCAN_V1")) {
         bool handled = false;
-        // FX_SCAN_V5=1: the 8-wave K-split scan (fx_scan5.hip), not yet the default
-        static const int v5 = getenv("FX_SCAN_V5") != nullptr ? atoi(getenv("FX_SCAN_V5")) : 0;
-        hipError_t e = v5 ? launch_scan_mfma5(st_dt, metric, p, s, v5 == 2, &handled)
-                          : launch_scan_mfma(st_dt, metric, p, s, &handled);
+        hipError_t e = launch_scan_mfma(st_dt, metric, p, s, &handled);
         if (handled) return e;
     }
     if (metric == L2) {
@@ -742,7 +956,9 @@ hipError_t launch_scan(int st_dt, int metric, const ScanParams& p, hipStream_t s
 
 template <int DT, int METRIC>
 static hipError_t refine_t(const RefineParams& p, hipStream_t s) {
-    if (p.prefetch > 1)
+    if (p.k > KP)
+        hipLaunchKernelGGL((k_refine_big<DT, METRIC>), dim3((unsigned)p.nq), dim3(BT_THREADS), 0, s, p);
+    else if (p.prefetch > 1)
         hipLaunchKernelGGL((k_refine<DT, METRIC, 4>), dim3((unsigned)((p.nq + 3) / 4)), dim3(256), 0, s, p);
     else
         hipLaunchKernelGGL((k_refine<DT, METRIC>), dim3((unsigned)((p.nq + 3) / 4)), dim3(256), 0, s, p);
@@ -761,40 +977,47 @@ hipError_t launch_refine(int st_dt, int metric, const RefineParams& p, hipStream
 }
 
 template <int DT, int METRIC>
-static void exact_scan_t(dim3 g, hipStream_t s, const char* codes, int row_bytes, int kdim, int64_t ntotal,
-                         const float* qf32, const int* qlist, int fb_splits, float* cd, int* ci) {
-    hipLaunchKernelGGL((k_exact_scan<DT, METRIC>), g, dim3(256), 0, s, codes, row_bytes, kdim, ntotal, qf32, qlist,
-                       fb_splits, cd, ci);
+static void fb_t(hipStream_t s, const char* codes, int row_bytes, int kdim, int64_t ntotal, const float* qf32,
+                 const int* n_flag, int k, float* cd, int* ci) {
+    hipLaunchKernelGGL((k_fb_scan<DT, METRIC>), dim3(FB_SCAN_GRID), dim3(BT_THREADS), 0, s, codes, row_bytes, kdim,
+                       ntotal, qf32, n_flag, k, cd, ci);
 }
 
 hipError_t launch_exact_fallback(int st_dt, int metric, const char* codes, int row_bytes, int kdim, int64_t ntotal,
-                                 const float* qf32, const int* qlist, int nlist, int k, int64_t id_offset,
-                                 float* cand_d, int* cand_i, int fb_splits, float* D, int64_t* I, hipStream_t s) {
-    if (nlist <= 0) return hipSuccess;
-    const dim3 g((unsigned)(nlist * fb_splits));
+                                 const float* qf32, const int* n_flag, int k, int64_t id_offset, float* cand_d,
+                                 int* cand_i, float* D, int64_t* I, hipStream_t s) {
     if (metric == L2) {
-        if (st_dt == F32) exact_scan_t<F32, L2>(g, s, codes, row_bytes, kdim, ntotal, qf32, qlist, fb_splits, cand_d, cand_i);
-        else if (st_dt == BF16) exact_scan_t<BF16, L2>(g, s, codes, row_bytes, kdim, ntotal, qf32, qlist, fb_splits, cand_d, cand_i);
-        else exact_scan_t<F16, L2>(g, s, codes, row_bytes, kdim, ntotal, qf32, qlist, fb_splits, cand_d, cand_i);
+        if (st_dt == F32) fb_t<F32, L2>(s, codes, row_bytes, kdim, ntotal, qf32, n_flag, k, cand_d, cand_i);
+        else if (st_dt == BF16) fb_t<BF16, L2>(s, codes, row_bytes, kdim, ntotal, qf32, n_flag, k, cand_d, cand_i);
+        else fb_t<F16, L2>(s, codes, row_bytes, kdim, ntotal, qf32, n_flag, k, cand_d, cand_i);
     } else {
-        if (st_dt == F32) exact_scan_t<F32, IP>(g, s, codes, row_bytes, kdim, ntotal, qf32, qlist, fb_splits, cand_d, cand_i);
-        else if (st_dt == BF16) exact_scan_t<BF16, IP>(g, s, codes, row_bytes, kdim, ntotal, qf32, qlist, fb_splits, cand_d, cand_i);
-        else exact_scan_t<F16, IP>(g, s, codes, row_bytes, kdim, ntotal, qf32, qlist, fb_splits, cand_d, cand_i);
+        if (st_dt == F32) fb_t<F32, IP>(s, codes, row_bytes, kdim, ntotal, qf32, n_flag, k, cand_d, cand_i);
+        else if (st_dt == BF16) fb_t<BF16, IP>(s, codes, row_bytes, kdim, ntotal, qf32, n_flag, k, cand_d, cand_i);
+        else fb_t<F16, IP>(s, codes, row_bytes, kdim, ntotal, qf32, n_flag, k, cand_d, cand_i);
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    const int per_query = fb_splits * 4 * KP;
-    const dim3 g2((unsigned)((nlist + 3) / 4));
     if (metric == L2)
-        hipLaunchKernelGGL(k_merge_exact<L2>, g2, dim3(256), 0, s, cand_d, cand_i, per_query, qlist, nlist, k, id_offset, D, I);
+        hipLaunchKernelGGL(k_fb_merge<L2>, dim3(FB_MERGE_GRID), dim3(BT_THREADS), 0, s, n_flag, ntotal, k, cand_d,
+                           cand_i, id_offset, D, I);
     else
-        hipLaunchKernelGGL(k_merge_exact<IP>, g2, dim3(256), 0, s, cand_d, cand_i, per_query, qlist, nlist, k, id_offset, D, I);
+        hipLaunchKernelGGL(k_fb_merge<IP>, dim3(FB_MERGE_GRID), dim3(BT_THREADS), 0, s, n_flag, ntotal, k, cand_d,
+                           cand_i, id_offset, D, I);
     return hipGetLastError();
 }
 
 hipError_t launch_merge_shards(int metric, int nshards, int64_t nq, int k, const float* D_in, const int64_t* I_in,
                                float* D_out, int64_t* I_out, hipStream_t s) {
     if (nq <= 0) return hipSuccess;
+    if (k > 64) {
+        if (metric == L2)
+            hipLaunchKernelGGL(k_merge_shards_big<L2>, dim3((unsigned)nq), dim3(BT_THREADS), 0, s, nshards, nq, k,
+                               D_in, I_in, D_out, I_out);
+        else
+            hipLaunchKernelGGL(k_merge_shards_big<IP>, dim3((unsigned)nq), dim3(BT_THREADS), 0, s, nshards, nq, k,
+                               D_in, I_in, D_out, I_out);
+        return hipGetLastError();
+    }
     const dim3 g((unsigned)((nq + 3) / 4));
     if (metric == L2)
         hipLaunchKernelGGL(k_merge_shards<L2>, g, dim3(256), 0, s, nshards, nq, k, D_in, I_in, D_out, I_out);

@@ -344,7 +344,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                 }
             });
             while (__builtin_amdgcn_ballot_w64(ovf)) {
-                compact_wave(lst_d, lst_i, cnt, tau, gtq, qw0, lane);
+                compact_wave(lst_d, lst_i, cnt, tau, p.share ? gtq : nullptr, qw0, lane);
                 ovf = false;
                 static_for<N>([&](auto NN) {
                     constexpr int n = decltype(NN)::value;

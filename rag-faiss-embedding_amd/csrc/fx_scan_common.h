@@ -1,5 +1,5 @@
 // fx_scan_common.h -- device helpers shared by the MFMA scan kernels
-// (fx_scan.hip: 4-wave k_scan_v4; fx_scan5.hip: 8-wave K-split k_scan_v5):
+// (fx_scan.hip: k_scan_v4; fx_scan_q32.hip: k_scan_q32):
 // LDS-DMA pieces with scalar bases, pinned LDS->operand reads, per-wave
 // candidate lists.
 #pragma once
@@ -88,7 +88,7 @@ __device__ __noinline__ void compact_wave(float* lst_d, int* lst_i, int* cnt, fl
             }
             if (lane == KP - 1) {
                 tau[q] = d;
-                atomicMin(gtq + qi, f2ord(d));
+                if (gtq) atomicMin(gtq + qi, f2ord(d));  // null: no cross-split pruning (k > KP)
             }
             if (lane == 0) cnt[q] = KP;
         }

@@ -105,6 +105,7 @@ class _FlatIndex:
         """``IndexFlat.add`` (faiss_store.py:46): append rows of ``x``."""
         if _is_device_tensor(x):
             assert x.dim() == 2 and x.shape[1] == self.d, "dimension mismatch"
+            assert x.device.index == self.device, f"tensor on cuda:{x.device.index}, index on cuda:{self.device}"
             x = x.contiguous()
             self._bind_stream(True)
             check(lib.fx_index_add(self._h, x.shape[0], ctypes.c_void_p(x.data_ptr()), _tensor_dtype(x),
@@ -123,7 +124,7 @@ class _FlatIndex:
             raise AssertionError("k must be positive")
         if k > _lib.MAX_K:
             # faiss pads with I = -1 / D = +-FLT_MAX beyond ntotal: serve k > MAX_K
-            # when the index holds at most MAX_K rows (e.g. faiss_store search(k=30)).
+            # when the index holds at most MAX_K rows.
             n = self.ntotal
             if n > _lib.MAX_K:
                 raise RuntimeError(f"k={k} > {_lib.MAX_K} is not supported for an index of {n} rows")
@@ -131,12 +132,18 @@ class _FlatIndex:
         if _is_device_tensor(x):
             t = _torch()
             assert x.dim() == 2 and x.shape[1] == self.d, "dimension mismatch"
+            assert x.device.index == self.device, f"queries on cuda:{x.device.index}, index on cuda:{self.device}"
             x = x.contiguous()
             nq = x.shape[0]
             if D is None:
                 D = t.empty((nq, k), dtype=t.float32, device=x.device)
             if I is None:
                 I = t.empty((nq, k), dtype=t.int64, device=x.device)
+            for name, a, dt in (("D", D, t.float32), ("I", I, t.int64)):
+                # the C side writes nq*k elements through the raw pointer
+                assert _is_device_tensor(a) and a.device == x.device, f"{name} must be on {x.device}"
+                assert a.dtype == dt and tuple(a.shape) == (nq, k) and a.is_contiguous(), \
+                    f"{name} must be a contiguous {dt} tensor of shape ({nq}, {k})"
             self._bind_stream(True)
             check(lib.fx_index_search(self._h, nq, ctypes.c_void_p(x.data_ptr()), _tensor_dtype(x),
                                       _lib.MEM_DEVICE, k, ctypes.c_void_p(D.data_ptr()),
@@ -147,6 +154,11 @@ class _FlatIndex:
         nq = x.shape[0]
         Dh = np.empty((nq, k), dtype=np.float32) if D is None else D
         Ih = np.empty((nq, k), dtype=np.int64) if I is None else I
+        for name, a, dt in (("D", Dh, np.float32), ("I", Ih, np.int64)):
+            # the C side writes nq*k elements through the raw pointer
+            assert isinstance(a, np.ndarray) and a.dtype == dt and a.shape == (nq, k) and \
+                a.flags.c_contiguous and a.flags.writeable, \
+                f"{name} must be a writeable C-contiguous {np.dtype(dt).name} array of shape ({nq}, {k})"
         self._bind_stream(False)
         check(lib.fx_index_search(self._h, nq, x.ctypes.data_as(ctypes.c_void_p), _lib.F32, _lib.MEM_HOST, k,
                                   Dh.ctypes.data_as(ctypes.c_void_p), Ih.ctypes.data_as(ctypes.c_void_p),

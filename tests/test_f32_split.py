@@ -1,4 +1,4 @@
-"""Split-fp32 scan (FX_F32_SPLIT=1): an fp32 index scanned through its
+"""Split-fp32 scan (the default for fp32 indexes): an fp32 index scanned through its
 [hi | lo] bf16 image with 3 bf16 MFMA products per term (fx_scan.hip, F32S).
 
 The scan key changes, the contract does not: results must equal the oracle's
@@ -8,10 +8,8 @@ scan's error bound, which for F32S adds the dropped lo*lo and residual terms:
     |key - exact| <= (2 gamma_{3K+1} + u)(|y|^2 + 2|x||y|) + 2 * 4.73e-5 |x||y|   (L2)
     |key - exact| <= (gamma_{3K+1} + u)|x||y| + 4.73e-5 |x||y|                    (IP)
 
-Not yet run on hardware: skipped unless FX_TEST_EXPERIMENTAL=1.
+(FX_F32_SPLIT=0 selects the fp32-MFMA scan instead; test_scan_keys pins that.)
 """
-import os
-
 import numpy as np
 import pytest
 
@@ -19,9 +17,7 @@ from oracle import cpu as C
 from oracle import flat_l2 as F
 from tests.test_gpu_parity import assert_parity
 
-pytestmark = [pytest.mark.gpu,
-              pytest.mark.skipif(os.environ.get("FX_TEST_EXPERIMENTAL") != "1",
-                                 reason="split-fp32 scan not yet validated on MI355X (FX_TEST_EXPERIMENTAL=1)")]
+pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(scope="module")

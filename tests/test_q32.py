@@ -3,11 +3,8 @@ own call shape (faiss_store.py:61 searches one query at a time).
 
 Same bar as every search: ids bit-exact with the oracle, distances within
 RTOL; plus the scan's key matrix against a float64 restatement, as in
-test_scan_keys.py.  Not yet run on hardware: skipped unless
-FX_TEST_EXPERIMENTAL=1.
+test_scan_keys.py.
 """
-import os
-
 import numpy as np
 import pytest
 import torch
@@ -16,9 +13,7 @@ from oracle import cpu as C
 from oracle import flat_l2 as F
 from tests.test_gpu_parity import assert_parity
 
-pytestmark = [pytest.mark.gpu,
-              pytest.mark.skipif(os.environ.get("FX_TEST_EXPERIMENTAL") != "1",
-                                 reason="small-batch scan not yet validated on MI355X (FX_TEST_EXPERIMENTAL=1)")]
+pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(scope="module")

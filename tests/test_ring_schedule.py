@@ -7,8 +7,8 @@ time.  Here the issue order of every kernel is replayed per wave and each
 wait is checked to retire exactly the stages it must, for every stage count
 per tile the kernels instantiate.
 
-Formulas restated from fx_scan.hip (k_scan_v4), fx_scan_q32.hip (k_scan_q32:
-same issue order as k_scan_v4) and fx_scan5.hip (k_scan_v5).
+Formulas restated from fx_scan.hip (k_scan_v4) and fx_scan_q32.hip
+(k_scan_q32: same issue order as k_scan_v4).
 """
 import pytest
 
@@ -50,10 +50,3 @@ def test_v4_and_q32_waits(ksteps):
     spt = ksteps // 2
     # prologue: vmcnt(12); loop: W = 8 + ((j+3)%SPT==0) + ((j+2)%SPT==0)
     _replay(spt, 4, True, 12, lambda j: 8 + ((j + 3) % spt == 0) + ((j + 2) % spt == 0))
-
-
-@pytest.mark.parametrize("ksteps", [8, 12, 16, 24])
-def test_v5_waits(ksteps):
-    spt = ksteps // 4
-    pro = 2 * (NS - 2) + sum(1 for s in (1, 2, 3) if s < NS - 1 and s % spt == 0)
-    _replay(spt, 2, True, pro, lambda j: 4 + ((j + NS - 3) % spt == 0) + ((j + NS - 2) % spt == 0))

@@ -36,6 +36,7 @@ def _scan_keys(fx, tmp_path, monkeypatch, cls, xb, xq, dtype):
     path = tmp_path / "keys.bin"
     monkeypatch.setenv("FX_SCAN_DBG", "32")
     monkeypatch.setenv("FX_SCAN_KEYS", str(path))
+    monkeypatch.setenv("FX_F32_SPLIT", "0")  # fp32 rows: pin the fp32-MFMA scan (test_f32_split pins F32S)
     d = xb.shape[1]
     ix = cls(d, dtype=dtype)
     ix.add(xb)

@@ -3,20 +3,16 @@ results out -- the reference's FAISSVectorStore.search call form
 (faiss_store.py:57-77) -- through one captured hipGraph per shape.
 
 Every replay must equal the oracle; the graph must be rebuilt whenever the
-index or the shape changes (add, reset, another k or nq).  Not yet run on
-hardware: skipped unless FX_TEST_EXPERIMENTAL=1.
+index or the shape changes (add, reset, another k or nq).  The graph holds the
+device-gated exact fallback too (FX_FORCE_FALLBACK=1 case).
 """
-import os
-
 import numpy as np
 import pytest
 
 from oracle import cpu as C
 from tests.test_gpu_parity import assert_parity
 
-pytestmark = [pytest.mark.gpu,
-              pytest.mark.skipif(os.environ.get("FX_TEST_EXPERIMENTAL") != "1",
-                                 reason="graph-replayed search not yet validated on MI355X (FX_TEST_EXPERIMENTAL=1)")]
+pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(scope="module")
@@ -73,3 +69,20 @@ def test_graph_store_single_queries(fx, monkeypatch):
         D, I = ix.search(xb[r:r + 1], 5)
         Dr, Ir = F.knn_inner_product(xb[r:r + 1], xb, 5)
         assert_parity(D, I, Dr, Ir)
+
+
+@pytest.mark.parametrize("k", [5, 100])
+def test_graph_replays_the_fallback(fx, monkeypatch, k):
+    """The captured graph holds the device-gated exact fallback: with every
+    query flagged (FX_FORCE_FALLBACK=1) each replay is still exact."""
+    monkeypatch.setenv("FX_SEARCH_GRAPH", "1")
+    monkeypatch.setenv("FX_FORCE_FALLBACK", "1")
+    rng = np.random.default_rng(13)
+    xb = rng.standard_normal((8000, 64)).astype(np.float32)
+    ix = fx.IndexFlatL2(64)
+    ix.add(xb)
+    for r in (1, 2, 4000, 7999):
+        D, I = ix.search(xb[r:r + 1] + 0.01, k)
+        Dr, Ir = C.knn_exact(xb[r:r + 1] + 0.01, xb, k)
+        assert_parity(D, I, Dr, Ir)
+        assert ix.last_fallbacks() == 1

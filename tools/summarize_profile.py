@@ -21,7 +21,7 @@ from collections import defaultdict
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-SCAN = os.environ.get("FX_PROFILE_KERNEL", "k_scan_v")  # k_scan_v4 / k_scan_v5
+SCAN = os.environ.get("FX_PROFILE_KERNEL", "k_scan_")  # k_scan_v4 / k_scan_q32
 
 
 def counters(path):

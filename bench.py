@@ -46,6 +46,10 @@ CONFIGS = {
     "b": (1_000_000, 384, "float32", 1_000, 10),
     "e": (100_000_000, 384, "float16", 10_000, 10),
 }
+# exact-oracle recall sample per config (>= 1000 queries where the
+# oracle allows; the full-corpus streaming oracle costs ~0.25 s per query on (d)
+# and ~1.2 s on (e) with 16 host cores)
+RECALL_QUERIES = {"d": 256, "b": 1000, "e": 32}
 TORCH_DT = {"float32": torch.float32, "bfloat16": torch.bfloat16, "float16": torch.float16}
 SHORT_DT = {"float32": "f32", "bfloat16": "bf16", "float16": "f16"}
 # MI355X_MICROARCH.md: dense MFMA peaks (TFLOP/s) and HBM3E peak (GB/s)
@@ -169,7 +173,8 @@ def main():
     ap.add_argument("--config", default="d", choices=sorted(CONFIGS))
     ap.add_argument("--nq", type=int, default=0, help="override query batch")
     ap.add_argument("--rows", type=int, default=0, help="override corpus rows (testing)")
-    ap.add_argument("--recall-queries", type=int, default=32)
+    ap.add_argument("--recall-queries", type=int, default=0,
+                    help="oracle recall sample (0: per config, SURVEY 8d: d 256, b 1000, e 32)")
     ap.add_argument("--cpu-rows", type=int, default=1_000_000)
     ap.add_argument("--cpu-queries", type=int, default=0, help="fixed CPU sample (0: auto-size)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="target CPU baseline sample time")
@@ -186,6 +191,8 @@ def main():
         dist.init_process_group("nccl", device_id=device)
 
     n_total, d, dtype, nq, k = CONFIGS[args.config]
+    if not args.recall_queries:
+        args.recall_queries = RECALL_QUERIES[args.config]
     if args.nq:
         nq = args.nq
     if args.rows:

@@ -93,9 +93,15 @@ struct FxIndex {
     // search workspace
     DevBuf qin, qf32, qop, qeps, cand_d, cand_i, dws, iws, flag, fbc_d, fbc_i, stage, gtau, trace, dbgbuf;
     // F32S scan image of an fp32 index (default; FX_F32_SPLIT=0 scans the fp32
-    // rows with fp32 MFMA instead): rows [0, split_rows) are current
-    DevBuf split;
-    int64_t split_rows = 0;
+    // rows with fp32 MFMA instead): rows [0, split_rows) are current.  L2
+    // indexes centre it (FX_CENTER=0: off): image rows fl(y - mu), their
+    // |.|^2 in cnorms (the scan's srcC), max in max_sq_bits[1]; mu = mean of a
+    // row sample, recomputed (and the image rebuilt) whenever ntotal has
+    // doubled since (mu_rows), so the centre follows the data at O(1)
+    // amortised cost per added row
+    DevBuf split, cnorms, centre, mu_part, qxn2;
+    int64_t split_rows = 0, mu_rows = 0;
+    bool centred = false;
     // FX_SEARCH_GRAPH=1: the search of a small host batch (the reference's
     // one-query call form) replayed as one hipGraph per shape, over pinned
     // host staging; `gkey` = the shape and every buffer the graph captured
@@ -166,10 +172,33 @@ hipError_t grow(FxIndex* h, int64_t need_rows) {
 // splits, so that a split's KP-list rarely holds fewer than all of its top-k
 // rows and the certification bound (the smallest full split's KP-th key)
 // lies far beyond the k-th distance
-void plan_scan(const FxIndex* h, int64_t nq, int k, ScanParams& p) {
+// split count whose live workgroups (one per CU: the scans' LDS) fill whole
+// rounds of 256 CUs best, with >= ~4 rounds and >= min_tiles tiles per split
+int fill_splits(int live_tiles, int eff_tiles, int n_ctiles, int min_tiles) {
+    const int max_splits = std::max(1, n_ctiles / min_tiles);
+    const int s0 = std::max(1, std::min(max_splits, (1024 + eff_tiles - 1) / eff_tiles));
+    int best = s0;
+    double best_eff = 0.0;
+    for (int s = s0; s <= std::min(max_splits, 4 * s0); ++s) {
+        const double live = (double)live_tiles * s;
+        const double rounds = std::ceil(live / 256.0);
+        const double eff = live / (rounds * 256.0);
+        if (eff > best_eff + 1e-9) { best_eff = eff; best = s; }
+        if (eff > 0.985) break;
+    }
+    return best;
+}
+
+// choose the scan kernel and its corpus splits per query tile
+// k > KP: no cross-split pruning (ScanParams.share = 0) and at least k/4
+// splits, so that a split's KP-list rarely holds fewer than all of its top-k
+// rows and the certification bound (the smallest full split's KP-th key)
+// lies far beyond the k-th distance
+void plan_scan(const FxIndex* h, int64_t nq, int k, int scan_dt, ScanParams& p) {
     p.n_qtiles = (int)((nq + TILE_Q - 1) / TILE_Q);
     p.n_ctiles = (int)((h->ntotal + TILE_R - 1) / TILE_R);
     p.q32_tiles = 0;
+    p.n_wtiles = 0;
     p.share = k <= KP ? 1 : 0;
     const int rb64 = h->row_bytes / 64;
     const char* q32_env = getenv("FX_SCAN_Q32");
@@ -182,24 +211,24 @@ void plan_scan(const FxIndex* h, int64_t nq, int k, ScanParams& p) {
         p.splits = std::max(1, std::min(p.n_ctiles / 4, 256 / p.q32_tiles));
         return;
     }
+    // large batches: the wide-tile scan (192 queries per workgroup; FX_SCAN_W
+    // = 0 / 1 forces it off / on where it has a kernel for the row width)
+    const char* w_env = getenv("FX_SCAN_W");
+    const bool want_w = w_env ? atoi(w_env) == 1 : false;
+    if (want_w && scan_w_supported(scan_dt, h->row_bytes)) {
+        const int qw = scan_w_queries();
+        p.n_wtiles = (int)((nq + qw - 1) / qw);
+        p.qt_per_xcd = p.n_wtiles >= 8 ? (p.n_wtiles + 7) / 8 : 0;
+        const int eff = p.qt_per_xcd > 0 ? 8 * p.qt_per_xcd : p.n_wtiles;
+        const int nct64 = (int)((h->ntotal + 63) / 64);
+        p.splits = fill_splits(p.n_wtiles, eff, nct64, 8);
+        if (k > KP) p.splits = std::max(p.splits, std::min(std::max(1, nct64 / 8), (k + 3) / 4));
+        return;
+    }
     p.qt_per_xcd = p.n_qtiles >= 8 ? (p.n_qtiles + 7) / 8 : 0;
     const int eff_q = p.qt_per_xcd > 0 ? 8 * p.qt_per_xcd : p.n_qtiles;
-    // One resident workgroup per CU (150 KiB LDS): pick the split count whose
-    // live workgroups (invalid query tiles exit at once) fill whole rounds of
-    // 256 CUs best, with >= ~4 rounds and >= 4 tiles per split.
-    const int max_splits = std::max(1, p.n_ctiles / 4);
-    const int s0 = std::max(1, std::min(max_splits, (1024 + eff_q - 1) / eff_q));
-    int best = s0;
-    double best_eff = 0.0;
-    for (int s = s0; s <= std::min(max_splits, 4 * s0); ++s) {
-        const double live = (double)p.n_qtiles * s;
-        const double rounds = std::ceil(live / 256.0);
-        const double eff = live / (rounds * 256.0);
-        if (eff > best_eff + 1e-9) { best_eff = eff; best = s; }
-        if (eff > 0.985) break;
-    }
-    if (k > KP) best = std::max(best, std::min(max_splits, (k + 3) / 4));
-    p.splits = best;
+    p.splits = fill_splits(p.n_qtiles, eff_q, p.n_ctiles, 4);
+    if (k > KP) p.splits = std::max(p.splits, std::min(std::max(1, p.n_ctiles / 4), (k + 3) / 4));
 }
 
 // k > KP: approx candidates the refine re-ranks exactly (k_refine_big)
@@ -222,14 +251,35 @@ hipError_t update_scan_image(FxIndex* h, bool* split) {
     if (!*split) return hipSuccess;
     hipStream_t s = h->stream();
     const void* old = h->split.p;
+    const void* old_n = h->cnorms.p;
     hipError_t e = h->split.ensure((size_t)h->cap_rows * h->row_bytes);
+    if (e == hipSuccess) e = h->cnorms.ensure((size_t)h->cap_rows * 4);
     if (e != hipSuccess) return e;
-    if (h->split.p != old || h->split_rows > h->ntotal) {  // fresh buffer: finite (zero) padding rows
-        e = hipMemsetAsync(h->split.p, 0, h->split.bytes, s);
-        if (e != hipSuccess) return e;
+    bool rebuild = h->split.p != old || h->cnorms.p != old_n || h->split_rows > h->ntotal;
+    const char* ce = getenv("FX_CENTER");
+    const bool centre = h->metric == L2 && !(ce && atoi(ce) == 0);
+    if (centre != h->centred) rebuild = true;
+    if (centre && (h->mu_rows == 0 || h->ntotal >= 2 * h->mu_rows)) {
+        // (re)centre on the current rows
+        if ((e = h->centre.ensure((size_t)h->kdim * 4)) != hipSuccess) return e;
+        if ((e = h->mu_part.ensure((size_t)MU_GROUPS * h->kdim * 8)) != hipSuccess) return e;
+        if ((e = launch_mu((const float*)h->codes, h->kdim, h->d, h->ntotal, (double*)h->mu_part.p, (float*)h->centre.p,
+                           s)) != hipSuccess)
+            return e;
+        h->mu_rows = h->ntotal;
+        rebuild = true;
+    }
+    h->centred = centre;
+    if (rebuild) {  // zero image (finite padding rows), +inf padding norms
+        if ((e = hipMemsetAsync(h->split.p, 0, h->split.bytes, s)) != hipSuccess) return e;
+        if ((e = hipMemsetD32Async((hipDeviceptr_t)h->cnorms.p, 0x7f800000u, h->cnorms.bytes / 4, s)) != hipSuccess)
+            return e;
+        if ((e = hipMemsetAsync(h->max_sq_bits + 1, 0, 4, s)) != hipSuccess) return e;
         h->split_rows = 0;
     }
-    e = launch_split_rows((const float*)h->codes, h->kdim, h->split_rows, h->ntotal, h->split.p, s);
+    e = launch_split_rows((const float*)h->codes, h->kdim, h->split_rows, h->ntotal,
+                          centre ? (const float*)h->centre.p : nullptr, h->split.p, (float*)h->cnorms.p,
+                          h->max_sq_bits + 1, s);
     if (e == hipSuccess) h->split_rows = h->ntotal;
     return e;
 }
@@ -237,7 +287,7 @@ hipError_t update_scan_image(FxIndex* h, bool* split) {
 int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int k, float* D, int64_t* I,
               int out_mem) {
     hipStream_t s = h->stream();
-    const int64_t nq_pad = round_up(nq, TILE_Q);
+    const int64_t nq_pad = round_up(nq, QPAD);
     const int qes = dtype_size(q_dtype);
     // queries -> device
     const void* qdev = q;
@@ -256,21 +306,23 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
     bool split = false;
     HIP_TRY(update_scan_image(h, &split));
     const int scan_dt = split ? (int)F32S : h->dtype;
+    HIP_TRY(h->qxn2.ensure((size_t)nq * 8));
     HIP_TRY(launch_prep_queries(qdev, q_dtype, nq, nq_pad, h->d, h->kdim, scan_dt, h->metric, (float*)h->qf32.p,
-                                qop, (float*)h->qeps.p, h->max_sq_bits, s));
+                                qop, (float*)h->qeps.p, h->max_sq_bits + (split ? 1 : 0),
+                                split && h->centred ? (const float*)h->centre.p : nullptr, (double*)h->qxn2.p, s));
 
     ScanParams sp;
-    plan_scan(h, nq, k, sp);
+    plan_scan(h, nq, k, scan_dt, sp);
     sp.codes = split ? (const char*)h->split.p : h->codes;
-    sp.norms = h->norms;
+    sp.norms = split ? (const float*)h->cnorms.p : h->norms;
     sp.ntotal = h->ntotal;
     sp.row_bytes = h->row_bytes;
     sp.qop = (const char*)qop;
     sp.nq = nq;
     sp.dbg = getenv("FX_SCAN_DBG") ? atoi(getenv("FX_SCAN_DBG")) : 0;
-    HIP_TRY(h->gtau.ensure((size_t)sp.n_qtiles * TILE_Q * 4));
+    HIP_TRY(h->gtau.ensure((size_t)nq_pad * 4));
     sp.gtau = (unsigned*)h->gtau.p;
-    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)sp.gtau, 0xff800000u, (size_t)sp.n_qtiles * TILE_Q, s));  // ord(+inf)
+    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)sp.gtau, 0xff800000u, (size_t)nq_pad, s));  // ord(+inf)
     const int cand_splits = sp.splits;  // one candidate list per (query, split)
     const size_t ncand = (size_t)sp.n_qtiles * cand_splits * TILE_Q * KP;
     HIP_TRY(h->cand_d.ensure(ncand * 4));
@@ -279,7 +331,9 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
     sp.cand_i = (int*)h->cand_i.p;
     // diagnostics: per-block placement/timing of the scan -> binary file
     const char* trace_path = getenv("FX_SCAN_TRACE");
-    const size_t grid = (size_t)(sp.q32_tiles > 0 ? sp.q32_tiles : sp.qt_per_xcd > 0 ? 8 * sp.qt_per_xcd : sp.n_qtiles) *
+    const size_t grid = (size_t)(sp.q32_tiles > 0 ? sp.q32_tiles
+                                 : sp.qt_per_xcd > 0 ? 8 * sp.qt_per_xcd
+                                 : sp.n_wtiles > 0 ? sp.n_wtiles : sp.n_qtiles) *
                         sp.splits;
     sp.trace = nullptr;
     sp.dbgbuf = nullptr;
@@ -328,6 +382,7 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
     rp.kdim = h->kdim;
     rp.qf32 = (const float*)h->qf32.p;
     rp.qeps = (const float*)h->qeps.p;
+    rp.qxn2 = (const double*)h->qxn2.p;
     rp.id_offset = h->id_offset;
     rp.D = Dd;
     rp.I = Id;
@@ -398,15 +453,17 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
 
 // Shape + every device buffer a captured search touches: the graph is valid
 // while all of them are unchanged
-std::vector<uint64_t> graph_key(const FxIndex* h, int64_t nq, int q_dtype, int k) {
+std::vector<uint64_t> graph_key(const FxIndex* h, int64_t nq, int q_dtype, int k, int scan_dt) {
     ScanParams sp;
-    plan_scan(h, nq, k, sp);
+    plan_scan(h, nq, k, scan_dt, sp);
     const char* se = getenv("FX_F32_SPLIT");  // (part of the key: unset and "1" both mean on)
     return {(uint64_t)nq, (uint64_t)q_dtype, (uint64_t)k, (uint64_t)h->ntotal, (uint64_t)h->id_offset,
             (uint64_t)(se ? atoi(se) : 1),
             (uint64_t)(getenv("FX_FORCE_FALLBACK") ? atoi(getenv("FX_FORCE_FALLBACK")) : 0),
-            (uint64_t)sp.splits, (uint64_t)sp.q32_tiles, (uint64_t)sp.qt_per_xcd,
+            (uint64_t)sp.splits, (uint64_t)sp.q32_tiles, (uint64_t)sp.qt_per_xcd, (uint64_t)sp.n_wtiles,
             (uint64_t)(uintptr_t)h->codes, (uint64_t)(uintptr_t)h->norms, (uint64_t)(uintptr_t)h->split.p,
+            (uint64_t)(uintptr_t)h->cnorms.p, (uint64_t)(uintptr_t)h->centre.p, (uint64_t)(uintptr_t)h->qxn2.p,
+            (uint64_t)h->centred,
             (uint64_t)(uintptr_t)h->qin.p, (uint64_t)(uintptr_t)h->qf32.p, (uint64_t)(uintptr_t)h->qop.p,
             (uint64_t)(uintptr_t)h->qeps.p, (uint64_t)(uintptr_t)h->gtau.p, (uint64_t)(uintptr_t)h->cand_d.p,
             (uint64_t)(uintptr_t)h->cand_i.p, (uint64_t)(uintptr_t)h->dws.p, (uint64_t)(uintptr_t)h->iws.p,
@@ -447,11 +504,11 @@ hipError_t graph_build(FxIndex* h, int64_t nq, int q_dtype, int k, bool split) {
     if (!h->ghnf && (e = hipHostMalloc((void**)&h->ghnf, 4, hipHostMallocDefault)) != hipSuccess) return e;
 
     const int scan_dt = split ? (int)F32S : h->dtype;
-    const int64_t nq_pad = round_up(nq, TILE_Q);
+    const int64_t nq_pad = round_up(nq, QPAD);
     ScanParams sp;
-    plan_scan(h, nq, k, sp);
+    plan_scan(h, nq, k, scan_dt, sp);
     sp.codes = split ? (const char*)h->split.p : h->codes;
-    sp.norms = h->norms;
+    sp.norms = split ? (const float*)h->cnorms.p : h->norms;
     sp.ntotal = h->ntotal;
     sp.row_bytes = h->row_bytes;
     sp.qop = (const char*)h->qop.p;
@@ -474,6 +531,7 @@ hipError_t graph_build(FxIndex* h, int64_t nq, int q_dtype, int k, bool split) {
     rp.kdim = h->kdim;
     rp.qf32 = (const float*)h->qf32.p;
     rp.qeps = (const float*)h->qeps.p;
+    rp.qxn2 = (const double*)h->qxn2.p;
     rp.id_offset = h->id_offset;
     rp.D = (float*)h->dws.p;
     rp.I = (int64_t*)h->iws.p;
@@ -488,9 +546,10 @@ hipError_t graph_build(FxIndex* h, int64_t nq, int q_dtype, int k, bool split) {
     hipError_t ce = hipMemcpyAsync(h->qin.p, h->ghq, qb, hipMemcpyHostToDevice, s);
     if (ce == hipSuccess)
         ce = launch_prep_queries(h->qin.p, q_dtype, nq, nq_pad, h->d, h->kdim, scan_dt, h->metric, (float*)h->qf32.p,
-                                 h->qop.p, (float*)h->qeps.p, h->max_sq_bits, s);
+                                 h->qop.p, (float*)h->qeps.p, h->max_sq_bits + (split ? 1 : 0),
+                                 split && h->centred ? (const float*)h->centre.p : nullptr, (double*)h->qxn2.p, s);
     if (ce == hipSuccess)
-        ce = hipMemsetD32Async((hipDeviceptr_t)sp.gtau, 0xff800000u, (size_t)sp.n_qtiles * TILE_Q, s);
+        ce = hipMemsetD32Async((hipDeviceptr_t)sp.gtau, 0xff800000u, (size_t)nq_pad, s);
     if (ce == hipSuccess) ce = launch_scan(scan_dt, h->metric, sp, s);
     if (ce == hipSuccess) ce = hipMemsetAsync(n_flag, 0, 4, s);
     if (ce == hipSuccess) ce = launch_refine(h->dtype, h->metric, rp, s);
@@ -512,7 +571,7 @@ hipError_t graph_build(FxIndex* h, int64_t nq, int q_dtype, int k, bool split) {
         (void)hipGetLastError();
         return e;
     }
-    h->gkey = graph_key(h, nq, q_dtype, k);
+    h->gkey = graph_key(h, nq, q_dtype, k, scan_dt);
     return hipSuccess;
 }
 
@@ -522,7 +581,7 @@ hipError_t graph_build(FxIndex* h, int64_t nq, int q_dtype, int k, bool split) {
 int graph_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int k, float* D, int64_t* I) {
     bool split = false;
     HIP_TRY(update_scan_image(h, &split));
-    if (h->gexec && graph_key(h, nq, q_dtype, k) == h->gkey) {
+    if (h->gexec && graph_key(h, nq, q_dtype, k, split ? (int)F32S : h->dtype) == h->gkey) {
         hipStream_t s = h->stream();
         memcpy(h->ghq, q, (size_t)nq * h->d * dtype_size(q_dtype));
         HIP_TRY(hipGraphLaunch(h->gexec, s));
@@ -607,7 +666,8 @@ void fx_index_free(FxIndex* h) {
         if (h->norms) (void)hipFree(h->norms);
         if (h->max_sq_bits) (void)hipFree(h->max_sq_bits);
         for (DevBuf* b : {&h->qin, &h->qf32, &h->qop, &h->qeps, &h->cand_d, &h->cand_i, &h->dws, &h->iws, &h->flag,
-                          &h->fbc_d, &h->fbc_i, &h->stage, &h->gtau, &h->trace, &h->dbgbuf, &h->split})
+                          &h->fbc_d, &h->fbc_i, &h->stage, &h->gtau, &h->trace, &h->dbgbuf, &h->split, &h->cnorms,
+                          &h->centre, &h->mu_part, &h->qxn2})
             b->release();
         graph_release(h);
         if (h->ghq) (void)hipHostFree(h->ghq);
@@ -758,13 +818,14 @@ int fx_index_reset(FxIndex* h) {
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard g(h->device);
     HIP_TRY(hipStreamSynchronize(h->stream()));
-    HIP_TRY(hipMemset(h->max_sq_bits, 0, 4));
+    HIP_TRY(hipMemset(h->max_sq_bits, 0, 8));
     if (h->codes && h->cap_rows > 0) {
         HIP_TRY(hipMemset(h->codes, 0, (size_t)h->cap_rows * h->row_bytes));
         HIP_TRY(hipMemsetD32((hipDeviceptr_t)h->norms, 0x7f800000u, (size_t)h->cap_rows));
     }
     h->ntotal = 0;
     h->split_rows = 0;
+    h->mu_rows = 0;
     return FX_OK;
 }
 

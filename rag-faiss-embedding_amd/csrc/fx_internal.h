@@ -60,7 +60,13 @@ struct ScanParams {
                                 // 32-query tiles (one workgroup per tile and split)
     int share;                  // 1: splits publish their KP-th key to gtau and prune with it
                                 // (k <= KP); 0: no cross-split pruning (k > KP, k_refine_big)
+    int n_wtiles;               // > 0: wide scan k_scan_w (fx_scan_w.hip) over this many tiles of
+                                // scan_w_queries() queries (qt_per_xcd then counts wide tiles)
 };
+
+// queries are zero-padded to a multiple of QPAD (a multiple of every scan's
+// query tile: 128, and the wide scan's 192)
+constexpr int QPAD = 768;
 
 struct RefineParams {
     const float* cand_d;   // scan output (approx keys)
@@ -73,6 +79,7 @@ struct RefineParams {
     int kdim;
     const float* qf32;     // [nq_pad][kdim] fp32 queries, zero padded
     const float* qeps;     // [nq] certification margin
+    const double* qxn2;    // [nq] |x - mu|^2 (mu: the scan image's centre, 0 if none)
     int64_t id_offset;
     float* D;              // [nq][k]
     int64_t* I;
@@ -104,14 +111,19 @@ extern thread_local bool g_graph_capture;
 hipError_t launch_convert_rows(const void* x, int x_dt, int64_t n, int d, void* codes_row0, int st_dt,
                                int kdim, float* norms_row0, unsigned* max_sq_bits, int normalize,
                                hipStream_t s);
+// mu: centre of a centred F32S image (null: none); qxn2[nq] <- |x - mu|^2 (fp64)
 hipError_t launch_prep_queries(const void* q, int q_dt, int64_t nq, int64_t nq_pad, int d, int kdim,
                                int st_dt, int metric, float* qf32, void* qop, float* qeps,
-                               const unsigned* max_sq_bits, hipStream_t s);
+                               const unsigned* max_sq_bits, const float* mu, double* qxn2, hipStream_t s);
 hipError_t launch_scan(int st_dt, int metric, const ScanParams& p, hipStream_t s);
 // fx_scan.hip: the MFMA scan; *handled = false when it has no kernel for p.row_bytes
 hipError_t launch_scan_mfma(int st_dt, int metric, const ScanParams& p, hipStream_t s, bool* handled);
 // fx_scan_q32.hip: the small-batch scan (p.q32_tiles > 0)
 hipError_t launch_scan_q32(int st_dt, int metric, const ScanParams& p, hipStream_t s, bool* handled);
+// fx_scan_w.hip: the wide-tile scan for large batches (p.n_wtiles > 0)
+hipError_t launch_scan_w(int st_dt, int metric, const ScanParams& p, hipStream_t s);
+bool scan_w_supported(int st_dt, int row_bytes);
+int scan_w_queries();
 hipError_t launch_refine(int st_dt, int metric, const RefineParams& p, hipStream_t s);
 // both fallback launches, always enqueued; they read the flagged count at
 // n_flag[0] (list at n_flag + 1) and do nothing when it is 0
@@ -122,7 +134,15 @@ hipError_t launch_exact_fallback(int st_dt, int metric, const char* codes, int r
 hipError_t launch_merge_shards(int metric, int nshards, int64_t nq, int k, const float* D_in,
                                const int64_t* I_in, float* D_out, int64_t* I_out, hipStream_t s);
 // fp32 code rows [r0, r1) -> their F32S scan image (same row stride)
-hipError_t launch_split_rows(const float* codes, int kdim, int64_t r0, int64_t r1, void* split, hipStream_t s);
+// (centred by mu when non-null), with the image rows' |v|^2 -> cnorms and their
+// maximum -> cmax_bits (atomicMax)
+hipError_t launch_split_rows(const float* codes, int kdim, int64_t r0, int64_t r1, const float* mu, void* split,
+                             float* cnorms, unsigned* cmax_bits, hipStream_t s);
+// mu[kdim] <- mean of a strided sample of <= MU_SAMPLE of the n fp32 rows
+// (part: MU_GROUPS * kdim doubles of scratch)
+constexpr int64_t MU_SAMPLE = 1 << 20;
+constexpr int MU_GROUPS = 64;
+hipError_t launch_mu(const float* codes, int kdim, int d, int64_t n, double* part, float* mu, hipStream_t s);
 hipError_t launch_synth(void* out, int64_t row0, int64_t n, int d, int dtype, uint64_t seed,
                         hipStream_t s);
 hipError_t launch_to_f32(const void* codes, int st_dt, int row_bytes, int64_t n, int d, float* out,

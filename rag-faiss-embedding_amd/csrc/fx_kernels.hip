@@ -136,26 +136,78 @@ __global__ __launch_bounds__(256) void k_convert_rows(const void* __restrict__ x
     if (threadIdx.x == 0 && bmax) atomicMax(max_sq_bits, bmax);
 }
 
-// fp32 rows -> F32S scan image: row r = [rn_bf16(v) for v in row | rn_bf16(v - hi)]
-// in the same row_bytes (kdim fp32 = 2 planes of kdim bf16); 4 values per thread
+// Centre of the F32S scan image (L2): mu = mean of a strided sample of up to
+// MU_SAMPLE rows.  Any mu gives correct results (distances are translation
+// invariant and the certification margin is computed for the centred
+// operands); a centre inside the data shrinks the operands' norms, and with
+// them the margin, by the spread-to-norm ratio of clustered embeddings.
+// Pass 1: block (column group of 64, row group g) sums its sample rows in fp64;
+// pass 2 sums the row groups in a fixed order (deterministic).
+__global__ __launch_bounds__(256) void k_mu_partial(const float* __restrict__ codes, int kdim, int64_t n,
+                                                    int64_t ns, double* __restrict__ part) {
+    __shared__ double red[4][64];
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63), sub = threadIdx.x >> 6, g = blockIdx.y;
+    double acc = 0.0;
+    if (c < kdim)
+        for (int64_t i = (int64_t)g * 4 + sub; i < ns; i += MU_GROUPS * 4)
+            acc += (double)codes[(i * n / ns) * kdim + c];
+    red[sub][threadIdx.x & 63] = acc;
+    __syncthreads();
+    if (sub == 0 && c < kdim)
+        part[(int64_t)g * kdim + c] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+}
+__global__ __launch_bounds__(256) void k_mu_finish(const double* __restrict__ part, int kdim, int d, int64_t ns,
+                                                   float* __restrict__ mu) {
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= kdim) return;
+    double s = 0.0;
+    for (int g = 0; g < MU_GROUPS; ++g) s += part[(int64_t)g * kdim + c];
+    mu[c] = c < d ? (float)(s / (double)ns) : 0.0f;  // padding columns stay 0
+}
+
+// fp32 rows -> F32S scan image: row r, v = fl(y - mu) (mu = 0 when null),
+// = [rn_bf16(v) for v in row | rn_bf16(v - hi)] in the same row_bytes (kdim
+// fp32 = 2 planes of kdim bf16); cnorms[r] = |v|^2 (fp32 fma chain per lane +
+// wave sum: the scan's srcC) and its maximum -> cmax_bits.  One wave per row.
 __global__ __launch_bounds__(256) void k_split_rows(const float* __restrict__ codes, int kdim, int64_t r0,
-                                                    int64_t r1, uint16_t* __restrict__ split) {
-    const int64_t n4 = (r1 - r0) * (int64_t)(kdim / 4);
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t row = r0 + i / (kdim / 4);
-        const int c = (int)(i % (kdim / 4)) * 4;
-        const float4 v = *(const float4*)(codes + row * kdim + c);
-        const float vv[4] = {v.x, v.y, v.z, v.w};
-        uint16_t hi[4], lo[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            hi[j] = f2bf(vv[j]);
-            lo[j] = f2bf(vv[j] - bf2f(hi[j]));
-        }
+                                                    int64_t r1, const float* __restrict__ mu,
+                                                    uint16_t* __restrict__ split, float* __restrict__ cnorms,
+                                                    unsigned* __restrict__ cmax_bits) {
+    __shared__ unsigned bmax;
+    if (threadIdx.x == 0) bmax = 0u;
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    unsigned my_max = 0u;
+    for (int64_t row = r0 + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < r1; row += (int64_t)gridDim.x * 4) {
+        const float* src = codes + row * kdim;
         uint16_t* out = split + row * (int64_t)(2 * kdim);
-        *(uint2*)(out + c) = make_uint2(hi[0] | ((uint32_t)hi[1] << 16), hi[2] | ((uint32_t)hi[3] << 16));
-        *(uint2*)(out + kdim + c) = make_uint2(lo[0] | ((uint32_t)lo[1] << 16), lo[2] | ((uint32_t)lo[3] << 16));
+        float sq = 0.0f;
+        for (int c = lane * 4; c < kdim; c += 256) {
+            const float4 v = *(const float4*)(src + c);
+            float vv[4] = {v.x, v.y, v.z, v.w};
+            if (mu) {
+                const float4 m = *(const float4*)(mu + c);
+                vv[0] -= m.x; vv[1] -= m.y; vv[2] -= m.z; vv[3] -= m.w;
+            }
+            uint16_t hi[4], lo[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                hi[j] = f2bf(vv[j]);
+                lo[j] = f2bf(vv[j] - bf2f(hi[j]));
+                sq = fmaf(vv[j], vv[j], sq);
+            }
+            *(uint2*)(out + c) = make_uint2(hi[0] | ((uint32_t)hi[1] << 16), hi[2] | ((uint32_t)hi[3] << 16));
+            *(uint2*)(out + kdim + c) = make_uint2(lo[0] | ((uint32_t)lo[1] << 16), lo[2] | ((uint32_t)lo[3] << 16));
+        }
+        sq = wave_sum_f32(sq);
+        if (lane == 0) {
+            cnorms[row] = sq;
+            my_max = max(my_max, __float_as_uint(sq));
+        }
     }
+    if (lane == 0 && my_max) atomicMax(&bmax, my_max);
+    __syncthreads();
+    if (threadIdx.x == 0 && bmax) atomicMax(cmax_bits, bmax);
 }
 
 // ---------------------------------------------------------------------------
@@ -165,20 +217,28 @@ __global__ __launch_bounds__(256) void k_prep_queries(const void* __restrict__ q
                                                       int64_t nq_pad, int d, int kdim, int st_dt, int metric,
                                                       float* __restrict__ qf32, void* __restrict__ qop,
                                                       float* __restrict__ qeps, const unsigned* __restrict__ max_sq_bits,
+                                                      const float* __restrict__ mu, double* __restrict__ qxn2,
                                                       double gamma) {
     const int lane = threadIdx.x & 63;
     const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= nq_pad) return;
     const bool live = r < nq;
-    double s = 0.0;
+    double s = 0.0, sc = 0.0;
     bool inexact = false;
     for (int c = lane; c < kdim; c += 64) {
         float v = (live && c < d) ? load_elem(q, r * d + c, q_dt) : 0.0f;
         qf32[r * (int64_t)kdim + c] = v;
+        // |x - mu|^2 for the certification (fp64 of the fp32 operands; mu = 0
+        // unless the F32S image is centred)
+        const double xm = (double)v - (mu ? (double)mu[c] : 0.0);
+        sc += xm * xm;
         if (st_dt == F32S) {
-            // split scan operand [hi plane | lo plane] of the pre-scaled query
-            // (x' - hi is exact in fp32: hi is within 2^-8 |x'| of x')
-            const float xs = v * (metric == L2 ? -2.0f : -1.0f);
+            // split scan operand [hi plane | lo plane] of the pre-scaled
+            // (centred) query (x' - hi is exact in fp32: hi is within 2^-8 |x'|
+            // of x')
+            const float vc = mu ? v - mu[c] : v;
+            s += (double)vc * (double)vc;
+            const float xs = vc * (metric == L2 ? -2.0f : -1.0f);
             const uint16_t hi = f2bf(xs);
             uint16_t* row = (uint16_t*)qop + r * (int64_t)(2 * kdim);
             row[c] = hi;
@@ -190,10 +250,12 @@ __global__ __launch_bounds__(256) void k_prep_queries(const void* __restrict__ q
             const float st = round_to(v, st_dt);
             inexact |= st != v;
             store_elem(qop, r * (int64_t)kdim + c, st_dt, st * (metric == L2 ? -2.0f : -1.0f));
+            s += (double)v * (double)v;
         }
-        s += (double)v * (double)v;
     }
     s = wave_sum_f64(s);
+    sc = wave_sum_f64(sc);
+    if (live && lane == 0) qxn2[r] = sc;
     inexact = __any(inexact);
     if (live && lane == 0) {
         // Worst-case bound on |approx - exact| of the scan's key for any row
@@ -201,16 +263,20 @@ __global__ __launch_bounds__(256) void k_prep_queries(const void* __restrict__ q
         // kdim terms (gamma = K u / (1 - K u)), one more rounding in the key
         // (u), and the query's rounding to the storage dtype (delta).
         const double u = 5.9604644775390625e-8;  // 2^-24
-        // M = the largest stored row norm, read on the device (add() never
-        // waits for the host to learn it)
+        // M = the largest row norm of the scanned operand (stored rows, or
+        // the centred F32S image), read on the device (add() never waits for
+        // the host to learn it); xn = the scanned query's norm
         const double xn = sqrt(s), M = sqrt((double)__uint_as_float(*max_sq_bits));
         // F32S: the split scan drops lo*lo and both residuals v - hi - lo;
         // per product <= 3 * 2^-16 (1 + 2^-7) |x_k||y_k|;
         // gamma then covers its 3 K products (launch_prep_queries)
         const double delta = st_dt == F32S ? 4.73e-5
                                            : (inexact ? (st_dt == BF16 ? 3.90625e-3 : 4.8828125e-4) : 0.0);
+        // centring (F32S): the operands are fl(y - mu), fl(x - mu): each
+        // product and square carries <= 2u + u^2 more (3u covers it)
+        const double cu = mu ? 3.0 * u : 0.0;
         double eps;
-        if (metric == L2) eps = (2.0 * gamma + u) * (M * M + 2.0 * xn * M) + 2.0 * delta * xn * M;
+        if (metric == L2) eps = (2.0 * gamma + u + cu) * (M * M + 2.0 * xn * M) + 2.0 * delta * xn * M;
         else eps = (gamma + u) * xn * M + delta * xn * M;
         qeps[r] = (float)(eps * 1.0625 + 1e-30);
     }
@@ -557,11 +623,8 @@ __global__ __launch_bounds__(256) void k_refine(RefineParams p) {
         const double v = __shfl(a, (lane & 3) * 16, 64);
         if ((lane >> 2) == r) ex = v;
     }
-    double xn2 = 0.0;
-    if (METRIC == L2) {
-        for (int c = lane; c < p.kdim; c += 64) xn2 = fma((double)xq[c], (double)xq[c], xn2);
-        xn2 = wave_sum_f64(xn2);
-    }
+    // |x - mu|^2 (mu: the scan image's centre, 0 if none), from k_prep_queries
+    const double xn2 = METRIC == L2 ? p.qxn2[q] : 0.0;
 
     // ---- phase 3: order by (fp32 exact key, id), write top-k, certify
     float key = FX_INF;
@@ -613,10 +676,9 @@ __global__ __launch_bounds__(BT_THREADS) void k_refine_big(RefineParams p) {
     __shared__ int ei[BT_MAXB];
     __shared__ BtState<int> st;
     __shared__ unsigned t_split;
-    __shared__ double red[BT_THREADS / 64];
     const int64_t q = blockIdx.x;
     if (q >= p.nq) return;
-    const int tid = threadIdx.x, lane = tid & 63;
+    const int tid = threadIdx.x;
     const int qtile = (int)(q / TILE_Q), qq = (int)(q % TILE_Q);
     const int K1 = p.k1, B = bt_cap(K1);
     if (tid == 0) t_split = f2ord(FX_INF);
@@ -665,14 +727,8 @@ __global__ __launch_bounds__(BT_THREADS) void k_refine_big(RefineParams p) {
         ed[t] = FX_INF;
         ei[t] = INT_MAX;
     }
-    double xn2 = 0.0;
-    if (METRIC == L2) {
-        for (int c = tid; c < p.kdim; c += BT_THREADS) xn2 = fma((double)xq[c], (double)xq[c], xn2);
-        xn2 = wave_sum_f64(xn2);
-        if (lane == 0) red[tid >> 6] = xn2;
-    }
-    bt_sort(ed, ei, n2);  // (syncs: ed/ei and red complete)
-    if (METRIC == L2) xn2 = red[0] + red[1] + red[2] + red[3];
+    bt_sort(ed, ei, n2);  // (syncs: ed/ei complete)
+    const double xn2 = METRIC == L2 ? p.qxn2[q] : 0.0;  // |x - mu|^2 (k_prep_queries)
 
     // phase 3: top-k out (faiss padding past the candidates), certification
     for (int t = tid; t < p.k; t += BT_THREADS) {
@@ -896,22 +952,32 @@ hipError_t launch_convert_rows(const void* x, int x_dt, int64_t n, int d, void* 
     return hipGetLastError();
 }
 
-hipError_t launch_split_rows(const float* codes, int kdim, int64_t r0, int64_t r1, void* split, hipStream_t s) {
+hipError_t launch_split_rows(const float* codes, int kdim, int64_t r0, int64_t r1, const float* mu, void* split,
+                             float* cnorms, unsigned* cmax_bits, hipStream_t s) {
     if (r1 <= r0) return hipSuccess;
-    hipLaunchKernelGGL(k_split_rows, dim3(grid_for((r1 - r0) * (kdim / 4), 256, 65536)), dim3(256), 0, s, codes,
-                       kdim, r0, r1, (uint16_t*)split);
+    hipLaunchKernelGGL(k_split_rows, dim3(grid_for(r1 - r0, 4, 65536)), dim3(256), 0, s, codes, kdim, r0, r1, mu,
+                       (uint16_t*)split, cnorms, cmax_bits);
+    return hipGetLastError();
+}
+
+hipError_t launch_mu(const float* codes, int kdim, int d, int64_t n, double* part, float* mu, hipStream_t s) {
+    if (n <= 0) return hipErrorInvalidValue;
+    const int64_t ns = n < MU_SAMPLE ? n : MU_SAMPLE;
+    hipLaunchKernelGGL(k_mu_partial, dim3((unsigned)((kdim + 63) / 64), MU_GROUPS), dim3(256), 0, s, codes, kdim, n,
+                       ns, part);
+    hipLaunchKernelGGL(k_mu_finish, dim3((unsigned)((kdim + 255) / 256)), dim3(256), 0, s, part, kdim, d, ns, mu);
     return hipGetLastError();
 }
 
 hipError_t launch_prep_queries(const void* q, int q_dt, int64_t nq, int64_t nq_pad, int d, int kdim, int st_dt,
                                int metric, float* qf32, void* qop, float* qeps, const unsigned* max_sq_bits,
-                               hipStream_t s) {
+                               const float* mu, double* qxn2, hipStream_t s) {
     const double u = 5.9604644775390625e-8;
     // terms accumulated by the scan's fp32 MFMA chain: K products (3 K for F32S) + srcC
     const double nt = st_dt == F32S ? 3.0 * kdim + 1.0 : (double)kdim;
     const double gamma = nt * u / (1.0 - nt * u);
     hipLaunchKernelGGL(k_prep_queries, dim3((unsigned)((nq_pad + 3) / 4)), dim3(256), 0, s, q, q_dt, nq, nq_pad, d,
-                       kdim, st_dt, metric, qf32, qop, qeps, max_sq_bits, gamma);
+                       kdim, st_dt, metric, qf32, qop, qeps, max_sq_bits, mu, qxn2, gamma);
     return hipGetLastError();
 }
 
@@ -929,6 +995,7 @@ static hipError_t scan_t(const ScanParams& p, hipStream_t s) {
 hipError_t launch_scan(int st_dt, int metric, const ScanParams& p, hipStream_t s) {
     // the MFMA scan (fx_scan.hip) covers every row width it has a register
     // layout for; other widths take the generic kernel above
+    if (p.n_wtiles > 0) return launch_scan_w(st_dt, metric, p, s);  // wide tiles (fx_scan_w.hip)
     if (p.q32_tiles > 0) {  // small batch: k_scan_q32 (fx_scan_q32.hip); the host planned for it
         bool handled = false;
         hipError_t e = launch_scan_q32(st_dt, metric, p, s, &handled);

@@ -29,9 +29,14 @@ def fx():
 
 
 @pytest.mark.parametrize("d", [128, 192, 256, 384])
-@pytest.mark.parametrize("metric", ["L2", "IP"])
-def test_split_scan_keys(fx, tmp_path, monkeypatch, d, metric):
+@pytest.mark.parametrize("metric,centre", [("L2", False), ("L2", True), ("IP", False)])
+def test_split_scan_keys(fx, tmp_path, monkeypatch, d, metric, centre):
+    """Raw F32S scan keys against the fp64 model within the certification
+    bound.  L2 images are centred by default (FX_CENTER): keys are then
+    |y - mu|^2 - 2 (x - mu).(y - mu), mu = the fp32 mean of the rows (all of
+    them below MU_SAMPLE), and the bound takes the centred norms + 3u."""
     monkeypatch.setenv("FX_F32_SPLIT", "1")
+    monkeypatch.setenv("FX_CENTER", "1" if centre else "0")
     monkeypatch.setenv("FX_SCAN_DBG", "32")
     path = tmp_path / "keys.bin"
     monkeypatch.setenv("FX_SCAN_KEYS", str(path))
@@ -39,6 +44,10 @@ def test_split_scan_keys(fx, tmp_path, monkeypatch, d, metric):
     n, nq = 1500 + d, 150
     xb = rng.standard_normal((n, d)).astype(np.float32)
     xq = rng.standard_normal((nq, d)).astype(np.float32)
+    if centre:  # a common offset: the case centring is for
+        off = (3.0 * rng.standard_normal(d)).astype(np.float32)
+        xb += off
+        xq += off
     ix = (fx.IndexFlatL2 if metric == "L2" else fx.IndexFlatIP)(d)
     ix.add(xb)
     ix.search(xq, 10)
@@ -46,6 +55,12 @@ def test_split_scan_keys(fx, tmp_path, monkeypatch, d, metric):
     kv = np.fromfile(path, dtype=np.float32).reshape(-1, ld)[:nq, :n].astype(np.float64)
     y = xb.astype(np.float64)
     x = xq.astype(np.float64)
+    cu = 0.0
+    if centre:
+        mu = y.mean(0).astype(np.float32).astype(np.float64)
+        y = (xb - mu.astype(np.float32)).astype(np.float64)
+        x = (xq - mu.astype(np.float32)).astype(np.float64)
+        cu = 3 * 2.0 ** -24
     dot = x @ y.T
     ny = (y ** 2).sum(1)[None, :]
     nx = np.sqrt((x ** 2).sum(1))[:, None]
@@ -54,7 +69,7 @@ def test_split_scan_keys(fx, tmp_path, monkeypatch, d, metric):
     g = K * u / (1 - K * u)
     if metric == "L2":
         ref = ny - 2 * dot
-        bound = (2 * g + u) * (ny + 2 * nx * np.sqrt(ny)) + 2 * 4.73e-5 * nx * np.sqrt(ny)
+        bound = (2 * g + u + cu) * (ny + 2 * nx * np.sqrt(ny)) + 2 * 4.73e-5 * nx * np.sqrt(ny)
     else:
         ref = -dot
         bound = (g + u) * nx * np.sqrt(ny) + 4.73e-5 * nx * np.sqrt(ny)

@@ -48,6 +48,7 @@ def test_q32_search_parity(fx, monkeypatch, dtype, d, nq, metric):
 def test_q32_keys(fx, tmp_path, monkeypatch, split):
     monkeypatch.setenv("FX_SCAN_Q32", "1")
     monkeypatch.setenv("FX_F32_SPLIT", split)
+    monkeypatch.setenv("FX_CENTER", "0")  # uncentred keys (test_f32_split pins the centred ones)
     monkeypatch.setenv("FX_SCAN_DBG", "32")
     path = tmp_path / "keys.bin"
     monkeypatch.setenv("FX_SCAN_KEYS", str(path))

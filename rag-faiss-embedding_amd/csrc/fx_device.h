@@ -116,21 +116,34 @@ __device__ __forceinline__ void glds16(const void* gsrc, char* lds_uniform) {
     __builtin_amdgcn_global_load_lds(gsrc, (__attribute__((address_space(3))) void*)lds_uniform, 16, 0, 0);
 }
 
-// blockIdx -> (query tile, corpus split).  With >= 8 query tiles the grid is
-// laid out so that, under the observed round-robin dispatch of blocks over the
-// 8 XCDs, each XCD group owns a fixed set of query tiles (their operand stays
-// in that XCD's L2) and all groups walk the corpus splits in the same order
-// (corpus rows are fetched from HBM about once and re-read from L2/MALL).
-// Placement only changes speed, never results.
-__device__ __forceinline__ void map_block(int b, const ScanParams& p, int& qtile, int& split) {
-    if (p.qt_per_xcd > 0) {
-        int xcd = b & 7, j = b >> 3;
+// blockIdx -> (query tile, corpus split) over `ntl` query tiles (the scan's
+// own tile: 128 queries for k_scan_v4, scan_w_queries() for k_scan_w).
+// Placement only changes speed, never results; both forms rely on the
+// observed round-robin dispatch of blocks over the 8 XCDs (b, b + 8, ... share
+// one XCD).
+//   place 0: with >= 8 query tiles each XCD group owns a fixed set of query
+//            tiles and all groups walk the corpus splits in the same order
+//            (corpus rows re-read from L2 / the Infinity Cache);
+//   place 1: corpus-partitioned -- XCD group x owns splits [x sx, (x+1) sx)
+//            for every query tile and walks them query-tile-major, so the
+//            ~32 blocks resident on an XCD stream the same split side by side
+//            and the XCD's L2 serves one corpus fetch to all of them.
+__device__ __forceinline__ void map_tile(int b, const ScanParams& p, int ntl, int& qtile, int& split) {
+    if (p.place == 1) {
+        const int xcd = b & 7, j = b >> 3;
+        qtile = j % ntl;
+        split = xcd * p.sx + j / ntl;
+    } else if (p.qt_per_xcd > 0) {
+        const int xcd = b & 7, j = b >> 3;
         qtile = xcd + 8 * (j % p.qt_per_xcd);
         split = j / p.qt_per_xcd;
     } else {
-        qtile = b % p.n_qtiles;
-        split = b / p.n_qtiles;
+        qtile = b % ntl;
+        split = b / ntl;
     }
+}
+__device__ __forceinline__ void map_block(int b, const ScanParams& p, int& qtile, int& split) {
+    map_tile(b, p, p.n_qtiles, qtile, split);
 }
 
 // diagnostics (FX_SCAN_TRACE): where and when each block ran

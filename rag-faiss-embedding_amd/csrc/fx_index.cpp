@@ -91,7 +91,7 @@ struct FxIndex {
     hipStream_t own_stream = nullptr;
     hipStream_t user_stream = nullptr;
     // search workspace
-    DevBuf qin, qf32, qop, qeps, cand_d, cand_i, dws, iws, flag, fbc_d, fbc_i, stage, gtau, trace, dbgbuf;
+    DevBuf qin, qf32, qop, qeps, cand_d, cand_i, dws, iws, flag, fbc_d, fbc_i, stage, gtau, trace, dbgbuf, stamps, pub;
     // F32S scan image of an fp32 index (default; FX_F32_SPLIT=0 scans the fp32
     // rows with fp32 MFMA instead): rows [0, split_rows) are current.  L2
     // indexes centre it (FX_CENTER=0: off): image rows fl(y - mu), their
@@ -199,6 +199,9 @@ void plan_scan(const FxIndex* h, int64_t nq, int k, int scan_dt, ScanParams& p) 
     p.n_ctiles = (int)((h->ntotal + TILE_R - 1) / TILE_R);
     p.q32_tiles = 0;
     p.n_wtiles = 0;
+    p.place = 0;
+    p.sx = 0;
+    p.pub = nullptr;
     p.share = k <= KP ? 1 : 0;
     const int rb64 = h->row_bytes / 64;
     const char* q32_env = getenv("FX_SCAN_Q32");
@@ -209,26 +212,49 @@ void plan_scan(const FxIndex* h, int64_t nq, int k, int scan_dt, ScanParams& p) 
         p.q32_tiles = (int)((nq + 31) / 32);
         p.qt_per_xcd = 0;
         p.splits = std::max(1, std::min(p.n_ctiles / 4, 256 / p.q32_tiles));
+        p.grid = p.q32_tiles * p.splits;
         return;
     }
     // large batches: the wide-tile scan (192 queries per workgroup; FX_SCAN_W
     // = 0 / 1 forces it off / on where it has a kernel for the row width)
     const char* w_env = getenv("FX_SCAN_W");
     const bool want_w = w_env ? atoi(w_env) == 1 : false;
-    if (want_w && scan_w_supported(scan_dt, h->row_bytes)) {
-        const int qw = scan_w_queries();
-        p.n_wtiles = (int)((nq + qw - 1) / qw);
-        p.qt_per_xcd = p.n_wtiles >= 8 ? (p.n_wtiles + 7) / 8 : 0;
-        const int eff = p.qt_per_xcd > 0 ? 8 * p.qt_per_xcd : p.n_wtiles;
-        const int nct64 = (int)((h->ntotal + 63) / 64);
-        p.splits = fill_splits(p.n_wtiles, eff, nct64, 8);
-        if (k > KP) p.splits = std::max(p.splits, std::min(std::max(1, nct64 / 8), (k + 3) / 4));
+    const bool wide = want_w && scan_w_supported(scan_dt, h->row_bytes);
+    if (wide) p.n_wtiles = (int)((nq + scan_w_queries() - 1) / scan_w_queries());
+    const int ntl = wide ? p.n_wtiles : p.n_qtiles;              // query tiles of the chosen scan
+    const int nct = wide ? (int)((h->ntotal + 63) / 64) : p.n_ctiles;  // its corpus tiles
+    const int min_tiles = wide ? 8 : 4;
+    // placement (map_tile): FX_SCAN_PLACE = 0 / 1 forces query-tile groups /
+    // the corpus-partitioned form
+    // default: corpus-partitioned for k_scan_v4 (fewer corpus fetches past L2:
+    // 257 vs 742 GB per config (d) launch, and ~2 % faster)
+    const char* pl_env = getenv("FX_SCAN_PLACE");
+    const int place = pl_env ? atoi(pl_env) : (wide ? 0 : 1);
+    if (place == 1 && ntl >= 8 && nct >= 8 * min_tiles) {
+        // XCD x owns 1/8 of the corpus for every query tile; sx splits per
+        // XCD so that its ntl * sx blocks fill whole rounds of its 32 CUs
+        p.place = 1;
+        p.qt_per_xcd = 0;
+        const int max_sx = std::max(1, nct / (8 * min_tiles));
+        int best = 1;
+        double best_eff = 0.0;
+        for (int sx = 1; sx <= std::min(max_sx, 16); ++sx) {
+            const double live = (double)ntl * sx;
+            const double eff = live / (std::ceil(live / 32.0) * 32.0);
+            if (eff > best_eff + 1e-9) { best_eff = eff; best = sx; }
+            if (eff > 0.985 && live >= 128) break;
+        }
+        if (k > KP) best = std::max(best, std::min(max_sx, ((k + 3) / 4 + 7) / 8));
+        p.sx = best;
+        p.splits = 8 * best;
+        p.grid = 8 * ntl * best;
         return;
     }
-    p.qt_per_xcd = p.n_qtiles >= 8 ? (p.n_qtiles + 7) / 8 : 0;
-    const int eff_q = p.qt_per_xcd > 0 ? 8 * p.qt_per_xcd : p.n_qtiles;
-    p.splits = fill_splits(p.n_qtiles, eff_q, p.n_ctiles, 4);
-    if (k > KP) p.splits = std::max(p.splits, std::min(std::max(1, p.n_ctiles / 4), (k + 3) / 4));
+    p.qt_per_xcd = ntl >= 8 ? (ntl + 7) / 8 : 0;
+    const int eff_q = p.qt_per_xcd > 0 ? 8 * p.qt_per_xcd : ntl;
+    p.splits = fill_splits(ntl, eff_q, nct, min_tiles);
+    if (k > KP) p.splits = std::max(p.splits, std::min(std::max(1, nct / min_tiles), (k + 3) / 4));
+    p.grid = eff_q * p.splits;
 }
 
 // k > KP: approx candidates the refine re-ranks exactly (k_refine_big)
@@ -323,6 +349,16 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
     HIP_TRY(h->gtau.ensure((size_t)nq_pad * 4));
     sp.gtau = (unsigned*)h->gtau.p;
     HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)sp.gtau, 0xff800000u, (size_t)nq_pad, s));  // ord(+inf)
+    // k_scan_v4's published per-split lists (the union threshold, see
+    // compact_wave): slow-path tiles 25.7 -> 16.5 %, config (d) -3 %;
+    // FX_SCAN_PUB=0 turns them off
+    const char* pub_env = getenv("FX_SCAN_PUB");
+    if (sp.share && sp.q32_tiles == 0 && sp.n_wtiles == 0 && sp.splits > 1 && !(pub_env && atoi(pub_env) == 0)) {
+        const size_t npub = (size_t)sp.n_qtiles * TILE_Q * sp.splits * KP;
+        HIP_TRY(h->pub.ensure(npub * 4));
+        HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)h->pub.p, 0x7f800000u, npub, s));  // +inf: no entry
+        sp.pub = (float*)h->pub.p;
+    }
     const int cand_splits = sp.splits;  // one candidate list per (query, split)
     const size_t ncand = (size_t)sp.n_qtiles * cand_splits * TILE_Q * KP;
     HIP_TRY(h->cand_d.ensure(ncand * 4));
@@ -331,12 +367,16 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
     sp.cand_i = (int*)h->cand_i.p;
     // diagnostics: per-block placement/timing of the scan -> binary file
     const char* trace_path = getenv("FX_SCAN_TRACE");
-    const size_t grid = (size_t)(sp.q32_tiles > 0 ? sp.q32_tiles
-                                 : sp.qt_per_xcd > 0 ? 8 * sp.qt_per_xcd
-                                 : sp.n_wtiles > 0 ? sp.n_wtiles : sp.n_qtiles) *
-                        sp.splits;
+    const size_t grid = (size_t)sp.grid;
     sp.trace = nullptr;
     sp.dbgbuf = nullptr;
+    sp.stamps = nullptr;
+    const char* stamp_path = getenv("FX_SCAN_STAMPS");
+    if (stamp_path) {
+        HIP_TRY(h->stamps.ensure(grid * 4 * 128));
+        HIP_TRY(hipMemsetAsync(h->stamps.p, 0, grid * 4 * 128, s));
+        sp.stamps = (unsigned long long*)h->stamps.p;
+    }
     const size_t nkeys = (size_t)sp.n_qtiles * TILE_Q * sp.n_ctiles * TILE_R;
     if ((sp.dbg & 32) && nkeys <= (size_t)1 << 26) {
         HIP_TRY(h->dbgbuf.ensure(nkeys * 4));
@@ -433,6 +473,14 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
             fclose(f);
         }
     }
+    if (sp.stamps) {
+        std::vector<unsigned long long> st(grid * 4 * 16);
+        HIP_TRY(hipMemcpy(st.data(), sp.stamps, grid * 4 * 128, hipMemcpyDeviceToHost));
+        if (FILE* f = fopen(stamp_path, "wb")) {
+            fwrite(st.data(), 8, st.size(), f);
+            fclose(f);
+        }
+    }
     if (sp.trace) {
         std::vector<unsigned long long> tr(grid * 4);
         HIP_TRY(hipMemcpy(tr.data(), sp.trace, grid * 32, hipMemcpyDeviceToHost));
@@ -461,6 +509,7 @@ std::vector<uint64_t> graph_key(const FxIndex* h, int64_t nq, int q_dtype, int k
             (uint64_t)(se ? atoi(se) : 1),
             (uint64_t)(getenv("FX_FORCE_FALLBACK") ? atoi(getenv("FX_FORCE_FALLBACK")) : 0),
             (uint64_t)sp.splits, (uint64_t)sp.q32_tiles, (uint64_t)sp.qt_per_xcd, (uint64_t)sp.n_wtiles,
+            (uint64_t)sp.place, (uint64_t)sp.sx, (uint64_t)sp.grid,
             (uint64_t)(uintptr_t)h->codes, (uint64_t)(uintptr_t)h->norms, (uint64_t)(uintptr_t)h->split.p,
             (uint64_t)(uintptr_t)h->cnorms.p, (uint64_t)(uintptr_t)h->centre.p, (uint64_t)(uintptr_t)h->qxn2.p,
             (uint64_t)h->centred,
@@ -519,6 +568,7 @@ hipError_t graph_build(FxIndex* h, int64_t nq, int q_dtype, int k, bool split) {
     sp.cand_i = (int*)h->cand_i.p;
     sp.trace = nullptr;
     sp.dbgbuf = nullptr;
+    sp.stamps = nullptr;
     int* n_flag = (int*)h->flag.p;
     RefineParams rp;
     rp.cand_d = sp.cand_d;
@@ -667,7 +717,7 @@ void fx_index_free(FxIndex* h) {
         if (h->max_sq_bits) (void)hipFree(h->max_sq_bits);
         for (DevBuf* b : {&h->qin, &h->qf32, &h->qop, &h->qeps, &h->cand_d, &h->cand_i, &h->dws, &h->iws, &h->flag,
                           &h->fbc_d, &h->fbc_i, &h->stage, &h->gtau, &h->trace, &h->dbgbuf, &h->split, &h->cnorms,
-                          &h->centre, &h->mu_part, &h->qxn2})
+                          &h->centre, &h->mu_part, &h->qxn2, &h->stamps, &h->pub})
             b->release();
         graph_release(h);
         if (h->ghq) (void)hipHostFree(h->ghq);

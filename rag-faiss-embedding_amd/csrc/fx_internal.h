@@ -62,6 +62,14 @@ struct ScanParams {
                                 // (k <= KP); 0: no cross-split pruning (k > KP, k_refine_big)
     int n_wtiles;               // > 0: wide scan k_scan_w (fx_scan_w.hip) over this many tiles of
                                 // scan_w_queries() queries (qt_per_xcd then counts wide tiles)
+    int place;                  // block placement (map_tile): 0 query-tile groups per XCD, 1
+                                // corpus-partitioned (XCD x owns splits [x sx, (x+1) sx))
+    int sx;                     // place 1: corpus splits per XCD (splits = 8 sx)
+    int grid;                   // workgroups of the scan launch
+    float* pub;                 // k_scan_v4 with share: [n_qtiles * TILE_Q][splits][KP] each split's
+                                // last compacted top-KP keys per query (null: not used)
+    unsigned long long* stamps; // diagnostics only (FX_SCAN_STAMPS, -DFX_ABLATION builds):
+                                // [grid][4 waves][16] per-wave cycle sums of the scan's phases
 };
 
 // queries are zero-padded to a multiple of QPAD (a multiple of every scan's

@@ -987,8 +987,7 @@ static hipError_t scan_t(const ScanParams& p, hipStream_t s) {
     hipError_t e = g_graph_capture ? hipSuccess : hipFuncSetAttribute((const void*)k_scan_topk<DT, METRIC>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, LDS_SCAN_BYTES);
     if (e != hipSuccess) return e;
-    const int grid = p.qt_per_xcd > 0 ? 8 * p.qt_per_xcd * p.splits : p.n_qtiles * p.splits;
-    hipLaunchKernelGGL((k_scan_topk<DT, METRIC>), dim3(grid), dim3(SCAN_THREADS), LDS_SCAN_BYTES, s, p);
+    hipLaunchKernelGGL((k_scan_topk<DT, METRIC>), dim3(p.grid), dim3(SCAN_THREADS), LDS_SCAN_BYTES, s, p);
     return hipGetLastError();
 }
 

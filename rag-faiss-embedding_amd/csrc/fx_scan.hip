@@ -35,6 +35,17 @@
 
 #include <stdlib.h>
 
+// bisect switches of experimental builds
+#ifndef FX_V4_MIDWAIT
+#define FX_V4_MIDWAIT 1   // 1: one lgkmcnt(0) mid-stage; 0: counted waits per MFMA pair (no gain measured)
+#endif
+#ifndef FX_V4_LATEMIN
+#define FX_V4_LATEMIN 1   // 1: group minima after the tile; 0: beside its last MFMAs (no gain measured)
+#endif
+#ifndef FX_V4_ATOMPUSH
+#define FX_V4_ATOMPUSH 0  // 1: push_group (branchy, one atomic per lane) instead of push_lean
+#endif
+
 namespace fx {
 
 constexpr int S_NS = 5;                         // ring slots (S_NS - 1 stages in flight)
@@ -48,13 +59,17 @@ constexpr int S_LD_OFF = S_RING_OFF + S_NS * S_STAGE;
 constexpr int S_LI_OFF = S_LD_OFF + TILE_Q * CAP * 4;
 constexpr int S_CNT_OFF = S_LI_OFF + TILE_Q * CAP * 4;
 constexpr int S_TAU_OFF = S_CNT_OFF + TILE_Q * 4;
-constexpr int S_LDS_BYTES = S_TAU_OFF + TILE_Q * 4;
+constexpr int S_TRASH_OFF = S_TAU_OFF + TILE_Q * 4;  // [4 waves][64 lanes] sink of the lean push
+constexpr int S_LDS_BYTES = S_TRASH_OFF + 4 * 256;
 static_assert(S_LDS_BYTES <= 160 * 1024, "LDS budget");
 
 // ABL: compile-time ablation switches of profiling builds (FX_ABLATION; 0 in
 // the product): 1 L2-resident corpus, 2 no corpus DMA, 4 no MFMA, 8 no
 // epilogue, 16 no per-stage barrier, 32 no mid-stage LDS wait -- timing only,
-// results invalid
+// results invalid; 64 per-wave s_memtime segment sums into p.stamps (results
+// valid, timing distorted by the stamps); 128 the stage's LDS-DMA pieces
+// issued as one burst after the first MFMA pair (results valid); 256 the
+// epilogue's fast path only (no pushes: results invalid)
 //
 // LN selects the shape of the corpus LDS-DMA pieces and of the LDS image:
 //   LN = 0: fragment-shaped pieces (16 rows x 64 B: each piece touches 16
@@ -94,11 +109,14 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
     int* cnt = (int*)(smem + S_CNT_OFF);
     float* tau = (float*)(smem + S_TAU_OFF);
     const int qw0 = wave * 32;  // this wave's queries (tile-local)
+    const uint32_t ld_off = lds_off(lst_d), li_off = lds_off(lst_i);
+    const uint32_t trash = lds_off(smem + S_TRASH_OFF) + (uint32_t)(wave * 256 + lane * 4);
     if (lane < 32) {
         cnt[qw0 + lane] = 0;
         tau[qw0 + lane] = KEY_MAX;
     }
     unsigned* gtq = p.gtau + q0 + qw0;
+    float* pubw = p.pub ? p.pub + (q0 + qw0) * p.splits * KP : nullptr;
 
     // queries -> AGPRs (B fragments), settled once before the DMA ring starts
     bfrag_t b[KSTEPS][N];
@@ -202,9 +220,15 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
     }
 
     int c = 0;  // ring slot of the current stage
+    // ABL & 64: per-wave cycle sums {stage wait + barrier, half 0, mid-stage
+    // LDS wait, half 1, epilogue, stages, slow-path tiles, slow-path cycles,
+    // compaction calls, compaction cycles, group pushes, -}
+    uint64_t stq[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t s_end = 0;
     for (int t = 0; t < ntiles; ++t) {
         float tr[N];
         unsigned gr[N];
+        float gmin[N][M];  // per (query column, 16-row group) minimum key of the tile
         static_for<SPT>([&](auto JJ) {
             constexpr int j = decltype(JJ)::value;
             constexpr bool LAST = j == SPT - 1;
@@ -221,11 +245,20 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
             // (4 corpus pieces each, + the norm piece where that stage
             // prefetched a tile's first stage)
             constexpr int W = 8 + ((j + 3) % SPT == 0) + ((j + 2) % SPT == 0);
+            uint64_t s_a = 0, s_b = 0, s_c = 0;
+            if constexpr (ABL & 64) {
+                s_a = __builtin_amdgcn_s_memtime();
+                if (j == 0 && s_end) stq[4] += s_a - s_end;
+            }
             if constexpr (ABL & 16)
                 asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(W) : "memory");
             else
                 asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(W) : "memory");
             __builtin_amdgcn_sched_barrier(0);
+            if constexpr (ABL & 64) {
+                s_b = __builtin_amdgcn_s_memtime();
+                stq[0] += s_b - s_a;
+            }
             // F32S (split fp32): stages j < SPT/2 hold the rows' hi plane and
             // take two passes (x_hi, then x_lo = query K-steps KH..); the lo
             // plane's stages take one pass against x_hi
@@ -252,8 +285,15 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                     ds_rd128<(m0 >> 1) * 256 + (m0 & 1) * 64>(yin[m0], na);
                     ds_rd128<(m1 >> 1) * 256 + (m1 & 1) * 64>(yin[m1], na);
                 }
-                if constexpr (m == 4) piece(std::integral_constant<int, 0>{}, JP{}, NXT{}, c4, tnext);
-                if constexpr (m == 6) piece(std::integral_constant<int, 1>{}, JP{}, NXT{}, c4, tnext);
+                if constexpr (ABL & 128) {
+                    if constexpr (m == 0) {
+                        static_for<4>([&](auto W) { piece(W, JP{}, NXT{}, c4, tnext); });
+                        if constexpr (jp == 0) piece(std::integral_constant<int, 4>{}, JP{}, NXT{}, c4, tnext);
+                    }
+                } else {
+                    if constexpr (m == 4) piece(std::integral_constant<int, 0>{}, JP{}, NXT{}, c4, tnext);
+                    if constexpr (m == 6) piece(std::integral_constant<int, 1>{}, JP{}, NXT{}, c4, tnext);
+                }
             });
             if constexpr (HI) {  // hi * x_lo (>= 14 MFMAs after each accumulator's previous write)
                 static_for<M>([&](auto MM) {
@@ -270,23 +310,53 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                 ds_rd32<0>(gr[0], ns);
                 ds_rd32<64>(gr[1], ns);
             }
-            if constexpr (!(ABL & 32)) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if constexpr (ABL & 64) {
+                s_c = __builtin_amdgcn_s_memtime();
+                stq[1] += s_c - s_b;
+            }
+            // (no stage-wide LDS wait here: half 1 waits for each Y[m] just
+            // before its MFMAs, counted)
+            if constexpr (FX_V4_MIDWAIT && !(ABL & 32)) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
+            if constexpr (ABL & 64) {
+                const uint64_t s_d = __builtin_amdgcn_s_memtime();
+                stq[2] += s_d - s_c;
+                s_c = s_d;
+            }
             // ---- half 1: Y MFMAs; read half 0 (X) of stage g+1 meanwhile
             const uint32_t rd_next = lds_base + S_RING_OFF + c1 * S_STAGE + rd_lane;
             static_for<M>([&](auto MM) {
                 constexpr int m = decltype(MM)::value;
+                // Y[m] landed: LDS ops issued after it are Y[m+1..M-1], in the
+                // last stage of a tile the 8 norm reads and 4 threshold reads
+                // of half 0, and the X reads of this half so far (2 per pair
+                // over its first four pairs); lgkmcnt holds at most 15
+                constexpr int LW = (M - 1 - m) + (LAST ? M + 2 * N : 0) + 2 * (m < M / 2 ? m : M / 2);
+                if constexpr (!(ABL & 32) && !FX_V4_MIDWAIT)
+                    asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(LW < 15 ? LW : 15) : "memory");
                 if constexpr (!(ABL & 4))
                     AsmMmaV<DT>::template mma2<0>(acc[m][0], acc[m][1], Y[m], b[kq0 + 1][0], b[kq0 + 1][1], yin[m]);
+                // last stage of the tile: acc[m - 2] is final (two MFMA pairs
+                // = 64 cycles past its last XDL write): its group minima now,
+                // beside the remaining MFMAs instead of after them
+                if constexpr (LAST && m >= 2 && !FX_V4_LATEMIN) {
+                    static_for<N>([&](auto NN) {
+                        constexpr int n = decltype(NN)::value;
+                        gmin[n][m - 2] = min4(acc[m - 2][n]);
+                    });
+                    __builtin_amdgcn_sched_barrier(0);
+                }
                 // half 0 of stage g+1: two reads per pair over the first four
                 // pairs (X[2m+1]'s last reader is >= 8 MFMAs back)
                 if constexpr (m < M / 2) {
                     ds_rd128<(2 * m) * 2048>(X[2 * m], rd_next);
                     ds_rd128<(2 * m + 1) * 2048>(X[2 * m + 1], rd_next);
                 }
-                if constexpr (m == 4) piece(std::integral_constant<int, 2>{}, JP{}, NXT{}, c4, tnext);
-                if constexpr (m == 5) piece(std::integral_constant<int, 3>{}, JP{}, NXT{}, c4, tnext);
-                if constexpr (m == 6 && jp == 0) piece(std::integral_constant<int, 4>{}, JP{}, NXT{}, c4, tnext);
+                if constexpr (!(ABL & 128)) {
+                    if constexpr (m == 4) piece(std::integral_constant<int, 2>{}, JP{}, NXT{}, c4, tnext);
+                    if constexpr (m == 5) piece(std::integral_constant<int, 3>{}, JP{}, NXT{}, c4, tnext);
+                    if constexpr (m == 6 && jp == 0) piece(std::integral_constant<int, 4>{}, JP{}, NXT{}, c4, tnext);
+                }
             });
             if constexpr (HI) {
                 static_for<M>([&](auto MM) {
@@ -296,13 +366,18 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                 });
             }
             __builtin_amdgcn_sched_barrier(0);
+            if constexpr (ABL & 64) {
+                s_end = __builtin_amdgcn_s_memtime();
+                stq[3] += s_end - s_c;
+                stq[5] += 1;
+            }
             rd_addr = rd_next;
             c = (int)c1;
         });
 
         // ---- epilogue of tile t: the accumulator holds the keys ------------
         acc_fence_v(acc);
-        if (p.dbgbuf) {  // diagnostics (FX_SCAN_DBG & 32): every key -> [nq_pad][cap rows]
+        if (__builtin_expect(p.dbgbuf != nullptr, 0)) {  // diagnostics (FX_SCAN_DBG & 32): every key -> [nq_pad][cap rows]
             float* keys = (float*)p.dbgbuf;
             const int64_t ld = (int64_t)p.n_ctiles * TILE_R;
 #pragma unroll
@@ -313,21 +388,28 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                     for (int i = 0; i < 4; ++i)
                         keys[(q0 + qloc[n]) * ld + (int64_t)(ct0 + t) * TILE_R + rl0 + 16 * m + i] = acc[m][n][i];
         }
+        // the tile's threshold reads (last stage, half 0) and the next
+        // stage's fragments have landed
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         float tn[N];
         tn[0] = qv0 ? fminf(tr[0], ord2f(gr[0])) : -FX_INF;
         tn[1] = qv1 ? fminf(tr[1], ord2f(gr[1])) : -FX_INF;
-        float gmin[N][M], mn[N];
+        float mn[N];
 #pragma unroll
         for (int n = 0; n < N; ++n) {
 #pragma unroll
-            for (int m = 0; m < M; ++m)
-                gmin[n][m] = fminf(fminf(acc[m][n][0], acc[m][n][1]), fminf(acc[m][n][2], acc[m][n][3]));
+            for (int m = FX_V4_LATEMIN ? 0 : M - 2; m < M; ++m) gmin[n][m] = min4(acc[m][n]);
             mn[n] = gmin[n][0];
 #pragma unroll
-            for (int m = 1; m < M; ++m) mn[n] = fminf(mn[n], gmin[n][m]);
+            for (int m = 1; m < M; ++m) mn[n] = __builtin_fminf(mn[n], gmin[n][m]);
         }
-        if (!(ABL & 8) && __builtin_amdgcn_ballot_w64(mn[0] <= tn[0] || mn[1] <= tn[1])) {
+        // unlikely: the slow path's code (pushes, compaction) is laid out
+        // after the loop, so the hot path runs through without a jump over it
+        // (the loop body then fits the instruction cache)
+        if (!(ABL & (8 | 256)) && __builtin_expect(__builtin_amdgcn_ballot_w64(mn[0] <= tn[0] || mn[1] <= tn[1]) != 0, 0)) {
             // slow path: some row beats a query's threshold
+            uint64_t s_sl = 0;
+            if constexpr (ABL & 64) s_sl = __builtin_amdgcn_s_memtime();
             const int trow0 = (ct0 + t) * TILE_R;
             const int rlim = p.ntotal < (int64_t)trow0 + TILE_R ? (int)p.ntotal : trow0 + TILE_R;
             unsigned pend[N] = {0u, 0u};
@@ -337,14 +419,26 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                 if (__builtin_amdgcn_ballot_w64(mn[n] <= tn[n])) {
                     static_for<M>([&](auto MM) {
                         constexpr int m = decltype(MM)::value;
-                        if (__builtin_amdgcn_ballot_w64(gmin[n][m] <= tn[n]))
-                            ovf |= push_group<M, N>(acc, n, m, 15u, tn[n], qloc[n], trow0 + rl0 + m * 16, rlim,
-                                                    lst_d, lst_i, cnt, pend[n]);
+                        if (__builtin_amdgcn_ballot_w64(gmin[n][m] <= tn[n])) {
+                            if constexpr (FX_V4_ATOMPUSH)
+                                ovf |= push_group<M, N>(acc, n, m, 15u, tn[n], qloc[n], trow0 + rl0 + m * 16, rlim,
+                                                        lst_d, lst_i, cnt, pend[n]);
+                            else
+                                ovf |= push_lean<M, N>(acc, n, m, 15u, tn[n], qloc[n], trow0 + rl0 + m * 16, rlim,
+                                                       ld_off, li_off, trash, cnt, pend[n]);
+                            if constexpr (ABL & 64) stq[10] += 1;
+                        }
                     });
                 }
             });
             while (__builtin_amdgcn_ballot_w64(ovf)) {
-                compact_wave(lst_d, lst_i, cnt, tau, p.share ? gtq : nullptr, qw0, lane);
+                uint64_t s_cp = 0;
+                if constexpr (ABL & 64) s_cp = __builtin_amdgcn_s_memtime();
+                compact_wave(lst_d, lst_i, cnt, tau, p.share ? gtq : nullptr, qw0, lane, pubw, p.splits, split);
+                if constexpr (ABL & 64) {
+                    stq[8] += 1;
+                    stq[9] += __builtin_amdgcn_s_memtime() - s_cp;
+                }
                 ovf = false;
                 static_for<N>([&](auto NN) {
                     constexpr int n = decltype(NN)::value;
@@ -355,10 +449,18 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                         constexpr int m = decltype(MM)::value;
                         const unsigned el = (pn >> (4 * m)) & 15u;
                         if (__builtin_amdgcn_ballot_w64(el != 0u))
-                            ovf |= push_group<M, N>(acc, n, m, el, tq, qloc[n], trow0 + rl0 + m * 16, rlim, lst_d,
-                                                    lst_i, cnt, pend[n]);
+                            if constexpr (FX_V4_ATOMPUSH)
+                                ovf |= push_group<M, N>(acc, n, m, el, tq, qloc[n], trow0 + rl0 + m * 16, rlim, lst_d,
+                                                        lst_i, cnt, pend[n]);
+                            else
+                                ovf |= push_lean<M, N>(acc, n, m, el, tq, qloc[n], trow0 + rl0 + m * 16, rlim, ld_off,
+                                                       li_off, trash, cnt, pend[n]);
                     });
                 });
+            }
+            if constexpr (ABL & 64) {
+                stq[6] += 1;
+                stq[7] += __builtin_amdgcn_s_memtime() - s_sl;
             }
         }
         // advance the tile bases (clamped: stages past the end re-read the last tile)
@@ -393,6 +495,10 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
         }
     }
     if (p.trace && tid == 0) p.trace[blockIdx.x * 4 + 3] = wall_clock64();
+    if constexpr (ABL & 64) {
+        if (p.stamps && lane == 0)
+            for (int i = 0; i < 12; ++i) p.stamps[((int64_t)blockIdx.x * 4 + wave) * 16 + i] = stq[i];
+    }
 }
 
 template <int DT, int METRIC, int KSTEPS, int ABL = 0, int LN = 0>
@@ -405,7 +511,7 @@ static hipError_t scan_v4_t(const ScanParams& p, hipStream_t s) {
     }
 #ifdef FX_ABLATION
     if constexpr (ABL == 0 && DT == BF16 && METRIC == L2 && KSTEPS == 24) {
-        switch (p.dbg & 63) {
+        switch (p.dbg & 511) {
             case 1: return scan_v4_t<DT, METRIC, KSTEPS, 1, LN>(p, s);
             case 2: return scan_v4_t<DT, METRIC, KSTEPS, 2, LN>(p, s);
             case 4: return scan_v4_t<DT, METRIC, KSTEPS, 4, LN>(p, s);
@@ -416,6 +522,10 @@ static hipError_t scan_v4_t(const ScanParams& p, hipStream_t s) {
             case 42: return scan_v4_t<DT, METRIC, KSTEPS, 42, LN>(p, s);
             case 58: return scan_v4_t<DT, METRIC, KSTEPS, 58, LN>(p, s);
             case 16: return scan_v4_t<DT, METRIC, KSTEPS, 16, LN>(p, s);
+            case 64: return scan_v4_t<DT, METRIC, KSTEPS, 64, LN>(p, s);
+            case 128: return scan_v4_t<DT, METRIC, KSTEPS, 128, LN>(p, s);
+            case 192: return scan_v4_t<DT, METRIC, KSTEPS, 192, LN>(p, s);
+            case 256: return scan_v4_t<DT, METRIC, KSTEPS, 256, LN>(p, s);
             default: break;
         }
     }
@@ -424,8 +534,7 @@ static hipError_t scan_v4_t(const ScanParams& p, hipStream_t s) {
                                    : hipFuncSetAttribute((const void*)k_scan_v4<DT, METRIC, KSTEPS, ABL, LN>,
                                                          hipFuncAttributeMaxDynamicSharedMemorySize, S_LDS_BYTES);
     if (e != hipSuccess) return e;
-    const int grid = p.qt_per_xcd > 0 ? 8 * p.qt_per_xcd * p.splits : p.n_qtiles * p.splits;
-    hipLaunchKernelGGL((k_scan_v4<DT, METRIC, KSTEPS, ABL, LN>), dim3(grid), dim3(SCAN_THREADS), S_LDS_BYTES, s, p);
+    hipLaunchKernelGGL((k_scan_v4<DT, METRIC, KSTEPS, ABL, LN>), dim3(p.grid), dim3(SCAN_THREADS), S_LDS_BYTES, s, p);
     return hipGetLastError();
 }
 

@@ -335,7 +335,7 @@ static hipError_t scan_q32_t(const ScanParams& p, hipStream_t s) {
     hipError_t e = g_graph_capture ? hipSuccess : hipFuncSetAttribute((const void*)k_scan_q32<DT, METRIC, KSTEPS>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, Q_LDS_BYTES);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_scan_q32<DT, METRIC, KSTEPS>), dim3(p.q32_tiles * p.splits), dim3(SCAN_THREADS),
+    hipLaunchKernelGGL((k_scan_q32<DT, METRIC, KSTEPS>), dim3(p.grid), dim3(SCAN_THREADS),
                        Q_LDS_BYTES, s, p);
     return hipGetLastError();
 }

@@ -164,20 +164,6 @@ __device__ __forceinline__ void acc_fence_w(f32x4 (&acc)[M][N]) {
         for (int n = 0; n < N; ++n) asm volatile("" : "+v"(acc[m][n]));
 }
 
-// blockIdx -> (wide query tile, corpus split): with >= 8 wide tiles each XCD
-// (round-robin dispatch) owns a fixed set of query tiles and all XCDs walk
-// the splits in the same order; placement only changes speed
-__device__ __forceinline__ void map_block_w(int b, const ScanParams& p, int& wt, int& split) {
-    if (p.qt_per_xcd > 0) {
-        const int xcd = b & 7, j = b >> 3;
-        wt = xcd + 8 * (j % p.qt_per_xcd);
-        split = j / p.qt_per_xcd;
-    } else {
-        wt = b % p.n_wtiles;
-        split = b / p.n_wtiles;
-    }
-}
-
 template <int DT, int METRIC, int KSTEPS, int M, int N, int SB, int NS, int CAPL>
 __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_w(ScanParams p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -210,7 +196,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_w(ScanParams p) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     int wt, split;
-    map_block_w(blockIdx.x, p, wt, split);
+    map_tile(blockIdx.x, p, p.n_wtiles, wt, split);
     if (wt >= p.n_wtiles) return;
     const int nct = (int)((p.ntotal + TR - 1) / TR);
     const int ct0 = (int)((int64_t)split * nct / p.splits);
@@ -526,8 +512,7 @@ static hipError_t scan_w_t(const ScanParams& p, hipStream_t s) {
                                    : hipFuncSetAttribute((const void*)k_scan_w<DT, METRIC, KSTEPS, M, N, SB, NS, CAPL>,
                                                          hipFuncAttributeMaxDynamicSharedMemorySize, L::BYTES);
     if (e != hipSuccess) return e;
-    const int grid = p.qt_per_xcd > 0 ? 8 * p.qt_per_xcd * p.splits : p.n_wtiles * p.splits;
-    hipLaunchKernelGGL((k_scan_w<DT, METRIC, KSTEPS, M, N, SB, NS, CAPL>), dim3(grid), dim3(SCAN_THREADS), L::BYTES,
+    hipLaunchKernelGGL((k_scan_w<DT, METRIC, KSTEPS, M, N, SB, NS, CAPL>), dim3(p.grid), dim3(SCAN_THREADS), L::BYTES,
                        s, p);
     return hipGetLastError();
 }

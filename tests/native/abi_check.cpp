@@ -1,0 +1,246 @@
+// abi_check.cpp -- host-sanitizer driver of the C ABI (include/fx_index.h).
+//
+// Built by `make -C rag-faiss-embedding_amd/csrc asan` with the host C++ of
+// fx_index.cpp compiled under -fsanitize=address,undefined (device code as
+// usual: GPU sanitizers are not available on this pool), and run on the GPU
+// box by tests/test_native_asan.py.  It walks every entry point through the
+// paths that size host / device buffers by hand: growth by repeated adds,
+// k <= 32 and k > 32 searches, host and device result buffers, the
+// graph-replayed small search, IxF2 write / read (fp32 and bf16 storage)
+// including truncated and foreign files, reset, and the argument-error paths.
+// Search results are checked against a float64 brute force on the host; any
+// mismatch or sanitizer report ends the program with a non-zero status.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <algorithm>
+#include <random>
+#include <string>
+#include <vector>
+
+#include <unistd.h>
+
+#include "../../include/fx_index.h"
+
+static int g_fail = 0;
+#define CHECK(cond, ...)                                                   \
+    do {                                                                   \
+        if (!(cond)) {                                                     \
+            fprintf(stderr, "FAIL %s:%d: ", __FILE__, __LINE__);           \
+            fprintf(stderr, __VA_ARGS__);                                  \
+            fprintf(stderr, " (last error: %s)\n", fx_last_error());       \
+            ++g_fail;                                                      \
+        }                                                                  \
+    } while (0)
+#define OK(call) CHECK((call) == FX_OK, "%s", #call)
+
+// top-k by float64 squared L2 (ties -> smaller id), the oracle's definition
+static void brute(const std::vector<float>& xb, int64_t n, const std::vector<float>& xq, int64_t nq, int d, int k,
+                  std::vector<int64_t>& I) {
+    I.assign((size_t)nq * k, -1);
+    std::vector<std::pair<float, int64_t>> all((size_t)n);
+    for (int64_t q = 0; q < nq; ++q) {
+        for (int64_t r = 0; r < n; ++r) {
+            double s = 0;
+            for (int c = 0; c < d; ++c) {
+                const double t = (double)xq[q * d + c] - (double)xb[r * d + c];
+                s += t * t;
+            }
+            all[r] = {(float)s, r};
+        }
+        const int kk = (int)std::min<int64_t>(k, n);
+        std::partial_sort(all.begin(), all.begin() + kk, all.end());
+        for (int j = 0; j < kk; ++j) I[q * k + j] = all[j].second;
+    }
+}
+
+static void search_and_check(FxIndex* ix, const std::vector<float>& xb, int64_t n, int d, int nq, int k,
+                             std::mt19937& rng, const char* what) {
+    std::normal_distribution<float> nd;
+    std::vector<float> xq((size_t)nq * d);
+    for (auto& v : xq) v = nd(rng);
+    std::vector<float> D((size_t)nq * k);
+    std::vector<int64_t> I((size_t)nq * k), Ir;
+    OK(fx_index_search(ix, nq, xq.data(), FX_F32, FX_MEM_HOST, k, D.data(), I.data(), FX_MEM_HOST));
+    brute(xb, n, xq, nq, d, k, Ir);
+    int bad = 0;
+    for (size_t i = 0; i < I.size(); ++i) bad += I[i] != Ir[i];
+    CHECK(bad == 0, "%s: %d of %zu ids differ from the float64 brute force", what, bad, I.size());
+    for (int q = 0; q < nq; ++q)
+        for (int j = (int)std::min<int64_t>(k, n); j < k; ++j)
+            CHECK(I[q * k + j] == -1 && D[q * k + j] == 3.4028234663852886e38f, "%s: padding slot", what);
+}
+
+int main() {
+    int ndev = 0;
+    OK(fx_device_count(&ndev));
+    if (ndev == 0) {
+        fprintf(stderr, "no GPU visible\n");
+        return 2;
+    }
+    std::mt19937 rng(7);
+    std::normal_distribution<float> nd;
+    const int d = 384;
+
+    // ---- argument errors -------------------------------------------------
+    FxIndex* bad = nullptr;
+    CHECK(fx_index_create(0, FX_F32, FX_METRIC_L2, 0, &bad) != FX_OK && bad == nullptr, "d = 0 accepted");
+    CHECK(fx_index_create(d, 7, FX_METRIC_L2, 0, &bad) != FX_OK, "bad dtype accepted");
+    CHECK(fx_index_read("/nonexistent/fx_abi_check.bin", FX_F32, 0, &bad) == FX_E_IO, "missing file");
+
+    FxIndex* ix = nullptr;
+    OK(fx_index_create(d, FX_F32, FX_METRIC_L2, 0, &ix));
+    {
+        float D[5];
+        int64_t I[5];
+        float q[d] = {0};
+        CHECK(fx_index_search(ix, 1, q, FX_F32, FX_MEM_HOST, 0, D, I, FX_MEM_HOST) != FX_OK, "k = 0 accepted");
+        CHECK(fx_index_search(ix, 1, q, FX_F32, FX_MEM_HOST, FX_MAX_K + 1, D, I, FX_MEM_HOST) != FX_OK,
+              "k > FX_MAX_K accepted");
+        CHECK(fx_index_add(ix, 3, nullptr, FX_F32, FX_MEM_HOST) != FX_OK, "null rows accepted");
+        // empty index: every slot is padding
+        OK(fx_index_search(ix, 1, q, FX_F32, FX_MEM_HOST, 5, D, I, FX_MEM_HOST));
+        for (int j = 0; j < 5; ++j) CHECK(I[j] == -1, "empty index slot %d", j);
+    }
+
+    // ---- growth by repeated (ragged) adds --------------------------------
+    std::vector<float> xb;
+    int64_t n = 0;
+    for (int64_t chunk : {1, 0, 127, 1000, 2049, 3}) {
+        std::vector<float> x((size_t)chunk * d);
+        for (auto& v : x) v = nd(rng);
+        OK(fx_index_add(ix, chunk, chunk ? x.data() : nullptr, FX_F32, FX_MEM_HOST));
+        xb.insert(xb.end(), x.begin(), x.end());
+        n += chunk;
+        int64_t nt = -1;
+        OK(fx_index_ntotal(ix, &nt));
+        CHECK(nt == n, "ntotal %lld != %lld", (long long)nt, (long long)n);
+    }
+    search_and_check(ix, xb, n, d, 1, 5, rng, "nq=1 k=5");
+    search_and_check(ix, xb, n, d, 77, 10, rng, "nq=77 k=10");
+    search_and_check(ix, xb, n, d, 300, 32, rng, "nq=300 k=32");
+    search_and_check(ix, xb, n, d, 9, 100, rng, "nq=9 k=100");
+    int64_t fb = -1;
+    OK(fx_index_last_fallbacks(ix, &fb));
+    CHECK(fb >= 0, "fallback count");
+
+    // ---- device queries and results --------------------------------------
+    {
+        const int nq = 40, k = 10;
+        std::vector<float> xq((size_t)nq * d);
+        for (auto& v : xq) v = nd(rng);
+        void *dq = nullptr, *dD = nullptr, *dI = nullptr;
+        CHECK(hipMalloc(&dq, xq.size() * 4) == hipSuccess, "hipMalloc");
+        CHECK(hipMalloc(&dD, (size_t)nq * k * 4) == hipSuccess, "hipMalloc");
+        CHECK(hipMalloc(&dI, (size_t)nq * k * 8) == hipSuccess, "hipMalloc");
+        CHECK(hipMemcpy(dq, xq.data(), xq.size() * 4, hipMemcpyHostToDevice) == hipSuccess, "H2D");
+        OK(fx_index_search(ix, nq, dq, FX_F32, FX_MEM_DEVICE, k, (float*)dD, (int64_t*)dI, FX_MEM_DEVICE));
+        std::vector<int64_t> I((size_t)nq * k), Ir;
+        CHECK(hipDeviceSynchronize() == hipSuccess, "sync");
+        CHECK(hipMemcpy(I.data(), dI, I.size() * 8, hipMemcpyDeviceToHost) == hipSuccess, "D2H");
+        brute(xb, n, xq, nq, d, k, Ir);
+        CHECK(I == Ir, "device-resident search ids");
+        (void)hipFree(dq);
+        (void)hipFree(dD);
+        (void)hipFree(dI);
+    }
+
+    // ---- graph-replayed small host search ---------------------------------
+    setenv("FX_SEARCH_GRAPH", "1", 1);
+    for (int rep = 0; rep < 3; ++rep) search_and_check(ix, xb, n, d, 1, 5, rng, "graph nq=1");
+    std::vector<float> extra((size_t)5 * d);
+    for (auto& v : extra) v = nd(rng);
+    OK(fx_index_add(ix, 5, extra.data(), FX_F32, FX_MEM_HOST));  // invalidates the captured graph
+    xb.insert(xb.end(), extra.begin(), extra.end());
+    n += 5;
+    search_and_check(ix, xb, n, d, 1, 5, rng, "graph after add");
+    unsetenv("FX_SEARCH_GRAPH");
+
+    // ---- IxF2 round trip, fp32 and bf16 storage ---------------------------
+    const std::string path = std::string(getenv("TMPDIR") ? getenv("TMPDIR") : "/tmp") + "/fx_abi_check.bin";
+    OK(fx_index_write(ix, path.c_str()));
+    for (int dt : {FX_F32, FX_BF16}) {
+        FxIndex* rd = nullptr;
+        OK(fx_index_read(path.c_str(), dt, 0, &rd));
+        if (!rd) continue;
+        int64_t nt = 0;
+        OK(fx_index_ntotal(rd, &nt));
+        CHECK(nt == n, "read ntotal");
+        std::vector<float> back((size_t)n * d);
+        OK(fx_index_reconstruct_n(rd, 0, n, back.data()));
+        if (dt == FX_F32) {
+            CHECK(memcmp(back.data(), xb.data(), back.size() * 4) == 0, "fp32 read is not byte-exact");
+            search_and_check(rd, xb, n, d, 33, 10, rng, "read fp32");
+        }
+        fx_index_free(rd);
+    }
+    // truncated copies of the file: every cut must fail cleanly
+    {
+        FILE* f = fopen(path.c_str(), "rb");
+        std::vector<char> bytes;
+        if (f) {
+            fseek(f, 0, SEEK_END);
+            bytes.resize((size_t)ftell(f));
+            fseek(f, 0, SEEK_SET);
+            CHECK(fread(bytes.data(), 1, bytes.size(), f) == bytes.size(), "read back");
+            fclose(f);
+        }
+        const std::string cut = path + ".cut";
+        for (size_t len : {(size_t)0, (size_t)3, (size_t)20, (size_t)44, (size_t)45, bytes.size() / 2, bytes.size() - 1}) {
+            FILE* g = fopen(cut.c_str(), "wb");
+            fwrite(bytes.data(), 1, len, g);
+            fclose(g);
+            FxIndex* rd = nullptr;
+            CHECK(fx_index_read(cut.c_str(), FX_F32, 0, &rd) != FX_OK && rd == nullptr, "truncated file (%zu B) accepted",
+                  len);
+        }
+        // a foreign fourcc
+        bytes[0] = 'X';
+        FILE* g = fopen(cut.c_str(), "wb");
+        fwrite(bytes.data(), 1, bytes.size(), g);
+        fclose(g);
+        FxIndex* rd = nullptr;
+        CHECK(fx_index_read(cut.c_str(), FX_F32, 0, &rd) != FX_OK, "foreign fourcc accepted");
+        remove(cut.c_str());
+    }
+    remove(path.c_str());
+
+    // ---- reset, then reuse --------------------------------------------------
+    OK(fx_index_reset(ix));
+    int64_t nt = -1;
+    OK(fx_index_ntotal(ix, &nt));
+    CHECK(nt == 0, "reset");
+    xb.assign(xb.begin(), xb.begin() + (size_t)500 * d);
+    OK(fx_index_add(ix, 500, xb.data(), FX_F32, FX_MEM_HOST));
+    search_and_check(ix, xb, 500, d, 20, 10, rng, "after reset");
+    fx_index_free(ix);
+
+    // ---- bf16 storage, inner product with normalisation -------------------
+    FxIndex* ip = nullptr;
+    OK(fx_index_create(256, FX_BF16, FX_METRIC_INNER_PRODUCT, 0, &ip));
+    OK(fx_index_set_normalize(ip, 1));
+    std::vector<float> y((size_t)4000 * 256);
+    for (auto& v : y) v = nd(rng);
+    OK(fx_index_add(ip, 4000, y.data(), FX_F32, FX_MEM_HOST));
+    {
+        std::vector<float> q((size_t)64 * 256), D(64 * 10);
+        std::vector<int64_t> I(64 * 10);
+        for (auto& v : q) v = nd(rng);
+        OK(fx_index_search(ip, 64, q.data(), FX_F32, FX_MEM_HOST, 10, D.data(), I.data(), FX_MEM_HOST));
+        for (int i = 0; i < 64; ++i)
+            for (int j = 1; j < 10; ++j) CHECK(D[i * 10 + j - 1] >= D[i * 10 + j], "IP order");
+    }
+    fx_index_free(ip);
+
+    if (g_fail) fprintf(stderr, "abi_check: %d failure(s)\n", g_fail);
+    else printf("abi_check ok\n");
+    fflush(stdout);
+    fflush(stderr);
+    // skip static destructors: the HIP runtime's own teardown frees memory
+    // through ASan's device allocator after the device runtime is unloaded
+    // (an ASan CHECK in ROCm code, not in this library)
+    _exit(g_fail ? 1 : 0);
+}

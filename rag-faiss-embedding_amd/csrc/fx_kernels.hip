@@ -136,6 +136,144 @@ __global__ __launch_bounds__(256) void k_convert_rows(const void* __restrict__ x
     if (threadIdx.x == 0 && bmax) atomicMax(max_sq_bits, bmax);
 }
 
+// The same conversion specialised on (input dtype, storage dtype, normalise)
+// for 16-B-aligned input rows: a wave takes R rows at a time (R * chunks per
+// row a multiple of 64 lanes where possible: 2 rows of 768 bf16), issues every
+// chunk load of those rows before converting any (up to CPL 16-B chunks in
+// flight per lane), and reduces the R row norms together.  Chunks partly or
+// wholly past d (row padding) take the element path.
+template <int XDT, int SDT, bool NORM>
+__global__ __launch_bounds__(256) void k_convert_rows_t(const void* __restrict__ x, int64_t n, int d,
+                                                        void* __restrict__ codes, int kdim, float* __restrict__ norms,
+                                                        unsigned* __restrict__ max_sq_bits, int R) {
+    constexpr int E = SDT == F32 ? 4 : 8;    // values per 16-B output chunk
+    constexpr int CPL = 4;                   // chunks per lane per wave iteration
+    constexpr int RMAX = 4;
+    __shared__ unsigned bmax;
+    if (threadIdx.x == 0) bmax = 0u;
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int nchunk = kdim / E;
+    const int tot = R * nchunk;  // <= 64 * CPL (host-checked)
+    const int64_t ngroups = (n + R - 1) / R;
+    const int64_t nwaves = (int64_t)gridDim.x * 4;
+    unsigned my_max = 0u;
+    for (int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); g < ngroups; g += nwaves) {
+        const int64_t r0 = g * R;
+        float v[CPL][E];
+        // all loads first
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+            const int c = lane + 64 * k;
+            const int rr = c / nchunk, cc = c - rr * nchunk;
+            const int64_t r = r0 + rr;
+            const int e0 = cc * E;
+            if (c < tot && r < n && e0 + E <= d) {
+                const char* src = (const char*)x + ((r * d + e0) * (XDT == F32 ? 4 : 2));
+                if constexpr (XDT == F32) {
+                    const float4 a = *(const float4*)src;
+                    v[k][0] = a.x; v[k][1] = a.y; v[k][2] = a.z; v[k][3] = a.w;
+                    if constexpr (E == 8) {
+                        const float4 b = *(const float4*)(src + 16);
+                        v[k][4] = b.x; v[k][5] = b.y; v[k][6] = b.z; v[k][7] = b.w;
+                    }
+                } else if constexpr (E == 8) {
+                    const uint4 a = *(const uint4*)src;
+                    const uint32_t w[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        const uint16_t hv = (uint16_t)(w[j >> 1] >> (16 * (j & 1)));
+                        v[k][j] = XDT == BF16 ? bf2f(hv) : h2f(hv);
+                    }
+                } else {
+                    const uint2 a = *(const uint2*)src;
+                    const uint32_t w[2] = {a.x, a.y};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const uint16_t hv = (uint16_t)(w[j >> 1] >> (16 * (j & 1)));
+                        v[k][j] = XDT == BF16 ? bf2f(hv) : h2f(hv);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < E; ++j)
+                    v[k][j] = (c < tot && r < n && e0 + j < d) ? load_elem(x, r * d + e0 + j, XDT) : 0.0f;
+            }
+        }
+        // per-row scale (opt-in normalisation: fp64 sum of the input squares)
+        float scale[RMAX];
+#pragma unroll
+        for (int q = 0; q < RMAX; ++q) scale[q] = 1.0f;
+        if constexpr (NORM) {
+            double sr[RMAX] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) {
+                const int rr = (lane + 64 * k) / nchunk;
+                double t = 0.0;
+#pragma unroll
+                for (int j = 0; j < E; ++j) t = fma((double)v[k][j], (double)v[k][j], t);
+#pragma unroll
+                for (int q = 0; q < RMAX; ++q) sr[q] += rr == q ? t : 0.0;
+            }
+#pragma unroll
+            for (int q = 0; q < RMAX; ++q) {
+                if (q < R) {
+                    const double s2 = wave_sum_f64(sr[q]);
+                    scale[q] = s2 > 0.0 ? (float)(1.0 / sqrt(s2)) : 1.0f;
+                }
+            }
+        }
+        // convert, store, |y|^2 of the stored values
+        float sq[RMAX] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+            const int c = lane + 64 * k;
+            const int rr = c / nchunk, cc = c - rr * nchunk;
+            const int64_t r = r0 + rr;
+            if (c >= tot || r >= n) continue;
+            float sc = scale[0];
+#pragma unroll
+            for (int q = 1; q < RMAX; ++q) sc = rr == q ? scale[q] : sc;
+            float part = 0.0f;
+            char* out = (char*)codes + r * (int64_t)kdim * (SDT == F32 ? 4 : 2) + cc * 16;
+            if constexpr (SDT == F32) {
+                float4 o;
+                o.x = v[k][0] * sc; o.y = v[k][1] * sc; o.z = v[k][2] * sc; o.w = v[k][3] * sc;
+                part = fmaf(o.x, o.x, part); part = fmaf(o.y, o.y, part);
+                part = fmaf(o.z, o.z, part); part = fmaf(o.w, o.w, part);
+                *(float4*)out = o;
+            } else {
+                uint32_t w[4];
+#pragma unroll
+                for (int j = 0; j < 8; j += 2) {
+                    const uint16_t h0 = SDT == BF16 ? f2bf(v[k][j] * sc) : f2h(v[k][j] * sc);
+                    const uint16_t h1 = SDT == BF16 ? f2bf(v[k][j + 1] * sc) : f2h(v[k][j + 1] * sc);
+                    const float s0 = SDT == BF16 ? bf2f(h0) : h2f(h0), s1 = SDT == BF16 ? bf2f(h1) : h2f(h1);
+                    part = fmaf(s0, s0, part);
+                    part = fmaf(s1, s1, part);
+                    w[j >> 1] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+                }
+                *(uint4*)out = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+#pragma unroll
+            for (int q = 0; q < RMAX; ++q) sq[q] += rr == q ? part : 0.0f;
+        }
+#pragma unroll
+        for (int q = 0; q < RMAX; ++q) {
+            if (q < R && r0 + q < n) {
+                const float t = wave_sum_f32(sq[q]);
+                if (lane == 0) {
+                    norms[r0 + q] = t;
+                    my_max = max(my_max, __float_as_uint(t));
+                }
+            }
+        }
+    }
+    if (lane == 0 && my_max) atomicMax(&bmax, my_max);
+    __syncthreads();
+    if (threadIdx.x == 0 && bmax) atomicMax(max_sq_bits, bmax);
+}
+
 // Centre of the F32S scan image (L2): mu = mean of a strided sample of up to
 // MU_SAMPLE rows.  Any mu gives correct results (distances are translation
 // invariant and the certification margin is computed for the centred
@@ -947,6 +1085,27 @@ hipError_t launch_convert_rows(const void* x, int x_dt, int64_t n, int d, void* 
                                float* norms_row0, unsigned* max_sq_bits, int normalize, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     const int vec = ((int64_t)d * (x_dt == F32 ? 4 : 2)) % 16 == 0 && ((uintptr_t)x & 15) == 0;
+    // rows per wave iteration: the fewest that fill whole 64-lane passes
+    const int nchunk = kdim / (st_dt == F32 ? 4 : 8);
+    int R = 1;
+    while (R < 4 && (R * nchunk) % 64 != 0) R *= 2;
+    if (vec && R * nchunk <= 256 && !getenv("FX_CONVERT_V1")) {
+        const unsigned grid = grid_for((n + R - 1) / R, 4, 65536);
+#define FX_CONV(XD, SD)                                                                                           \
+        if (x_dt == XD && st_dt == SD) {                                                                         \
+            if (normalize)                                                                                       \
+                hipLaunchKernelGGL((k_convert_rows_t<XD, SD, true>), dim3(grid), dim3(256), 0, s, x, n, d,       \
+                                   codes_row0, kdim, norms_row0, max_sq_bits, R);                               \
+            else                                                                                                 \
+                hipLaunchKernelGGL((k_convert_rows_t<XD, SD, false>), dim3(grid), dim3(256), 0, s, x, n, d,      \
+                                   codes_row0, kdim, norms_row0, max_sq_bits, R);                               \
+            return hipGetLastError();                                                                            \
+        }
+        FX_CONV(F32, F32) FX_CONV(F32, BF16) FX_CONV(F32, F16)
+        FX_CONV(BF16, F32) FX_CONV(BF16, BF16) FX_CONV(BF16, F16)
+        FX_CONV(F16, F32) FX_CONV(F16, BF16) FX_CONV(F16, F16)
+#undef FX_CONV
+    }
     hipLaunchKernelGGL(k_convert_rows, dim3(grid_for(n, 4, 65536)), dim3(256), 0, s, x, x_dt, n, d, codes_row0,
                        st_dt, kdim, norms_row0, max_sq_bits, normalize, vec);
     return hipGetLastError();

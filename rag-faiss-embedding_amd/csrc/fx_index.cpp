@@ -202,6 +202,7 @@ void plan_scan(const FxIndex* h, int64_t nq, int k, int scan_dt, ScanParams& p) 
     p.place = 0;
     p.sx = 0;
     p.pub = nullptr;
+    p.prune_rank = KP;
     p.share = k <= KP ? 1 : 0;
     const int rb64 = h->row_bytes / 64;
     const char* q32_env = getenv("FX_SCAN_Q32");
@@ -358,6 +359,11 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
         HIP_TRY(h->pub.ensure(npub * 4));
         HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)h->pub.p, 0x7f800000u, npub, s));  // +inf: no entry
         sp.pub = (float*)h->pub.p;
+        // union bound taken at rank max(2k, 16) (<= KP): tighter pruning; the
+        // refine's certification bound is capped by the final threshold
+        const char* rk_env = getenv("FX_PRUNE_RANK");
+        sp.prune_rank = rk_env ? atoi(rk_env) : std::max(2 * k, 16);
+        sp.prune_rank = std::max(k, std::min(KP, sp.prune_rank));
     }
     const int cand_splits = sp.splits;  // one candidate list per (query, split)
     const size_t ncand = (size_t)sp.n_qtiles * cand_splits * TILE_Q * KP;
@@ -431,6 +437,7 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
     rp.prefetch = sp.q32_tiles > 0 ? 4 : 1;
     rp.k1 = big_k1(k);
     rp.force_fb = getenv("FX_FORCE_FALLBACK") ? atoi(getenv("FX_FORCE_FALLBACK")) : 0;
+    rp.gtau = sp.share ? sp.gtau : nullptr;
     HIP_TRY(launch_refine(h->dtype, h->metric, rp, s));
     if (h->profile) {
         HIP_TRY(hipEventRecord(e2, s));
@@ -590,6 +597,7 @@ hipError_t graph_build(FxIndex* h, int64_t nq, int q_dtype, int k, bool split) {
     rp.prefetch = sp.q32_tiles > 0 ? 4 : 1;
     rp.k1 = big_k1(k);
     rp.force_fb = getenv("FX_FORCE_FALLBACK") ? atoi(getenv("FX_FORCE_FALLBACK")) : 0;
+    rp.gtau = sp.share ? sp.gtau : nullptr;
 
     if ((e = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal)) != hipSuccess) return e;
     g_graph_capture = true;

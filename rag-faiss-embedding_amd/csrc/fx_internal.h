@@ -66,6 +66,7 @@ struct ScanParams {
                                 // corpus-partitioned (XCD x owns splits [x sx, (x+1) sx))
     int sx;                     // place 1: corpus splits per XCD (splits = 8 sx)
     int grid;                   // workgroups of the scan launch
+    int prune_rank;             // rank of the union bound published to gtau (compact_wave)
     float* pub;                 // k_scan_v4 with share: [n_qtiles * TILE_Q][splits][KP] each split's
                                 // last compacted top-KP keys per query (null: not used)
     unsigned long long* stamps; // diagnostics only (FX_SCAN_STAMPS, -DFX_ABLATION builds):
@@ -96,6 +97,8 @@ struct RefineParams {
     int prefetch;          // > 1: phase-1 loads issued 4 chunks at a time (small-batch scan)
     int k1;                // k > KP: approx candidates re-ranked exactly (2k, <= 2 FX_BIG_K)
     int force_fb;          // test hook (FX_FORCE_FALLBACK=1): flag every query -> exact fallback
+    const unsigned* gtau;  // k <= KP: the scan's final shared thresholds (ordered bits): every row a split
+                           // dropped lies above it, so it caps the certification bound; null: unused
 };
 
 // exact fallback (k_fb_scan / k_fb_merge): corpus splits per flagged query,

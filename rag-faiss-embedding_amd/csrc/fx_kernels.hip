@@ -782,7 +782,10 @@ __global__ __launch_bounds__(256) void k_refine(RefineParams p) {
     // key_k < td (+|x|^2 for L2) - eps.
     if (nvalid >= KP) {
         const float kth = __shfl(key, p.k - 1, 64);
-        const double bound = (METRIC == L2 ? (double)td + xn2 : (double)td) - (double)p.qeps[q];
+        // a split may also have pruned with the shared threshold (a bound on
+        // a rank below KP, compact_wave): dropped rows lie above min(td, it)
+        const float tb = p.gtau ? fminf(td, ord2f(p.gtau[q])) : td;
+        const double bound = (METRIC == L2 ? (double)tb + xn2 : (double)tb) - (double)p.qeps[q];
         const double kup = (double)kth + fabs((double)kth) * 2.384185791015625e-7;  // + 2 ulp
         if (!(kup < bound) && lane == 0 && !p.force_fb) {
             const int pos = atomicAdd(p.n_flag, 1);

@@ -412,6 +412,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
             if constexpr (ABL & 64) s_sl = __builtin_amdgcn_s_memtime();
             const int trow0 = (ct0 + t) * TILE_R;
             const int rlim = p.ntotal < (int64_t)trow0 + TILE_R ? (int)p.ntotal : trow0 + TILE_R;
+            {
             unsigned pend[N] = {0u, 0u};
             bool ovf = false;
             static_for<N>([&](auto NN) {
@@ -434,7 +435,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
             while (__builtin_amdgcn_ballot_w64(ovf)) {
                 uint64_t s_cp = 0;
                 if constexpr (ABL & 64) s_cp = __builtin_amdgcn_s_memtime();
-                compact_wave(lst_d, lst_i, cnt, tau, p.share ? gtq : nullptr, qw0, lane, pubw, p.splits, split);
+                compact_wave(lst_d, lst_i, cnt, tau, p.share ? gtq : nullptr, qw0, lane, pubw, p.splits, split, p.prune_rank);
                 if constexpr (ABL & 64) {
                     stq[8] += 1;
                     stq[9] += __builtin_amdgcn_s_memtime() - s_cp;
@@ -457,6 +458,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                                                        li_off, trash, cnt, pend[n]);
                     });
                 });
+            }
             }
             if constexpr (ABL & 64) {
                 stq[6] += 1;

@@ -72,14 +72,15 @@ __device__ __forceinline__ void ds_rd32(T& d, uint32_t addr) {
     asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(d) : "v"(addr), "i"(OFF) : "memory");
 }
 
-// A bound on the KP-th smallest key of the union of `nl` published lists
+// A bound on the rank-th smallest key of the union of `nl` published lists
 // (float keys, `stride` apart, the first 16 entries of each read: 4 per lane
 // for up to 16 lists): the smallest v found by 8 bisection steps over the
-// ordered-uint range [lo, hi] such that at least KP entries are <= v (hi =
-// the caller's own KP-th key, which already qualifies).  Counting entries is
-// a valid lower bound on the rows below v (see compact_wave), so any v the
-// bisection accepts bounds the global KP-th key.
-__device__ __forceinline__ unsigned union_kth(const float* lists, int nl, int stride, unsigned hi, int lane) {
+// ordered-uint range [lo, hi] such that at least `rank` entries are <= v (hi
+// = the caller's own rank-th key, which already qualifies).  Counting entries
+// is a valid lower bound on the rows below v (see compact_wave), so any v the
+// bisection accepts bounds the global rank-th key.
+__device__ __forceinline__ unsigned union_kth(const float* lists, int nl, int stride, unsigned hi, int rank,
+                                              int lane) {
     unsigned kv[4];
     unsigned lo = 0xFFFFFFFFu;
 #pragma unroll
@@ -100,7 +101,7 @@ __device__ __forceinline__ unsigned union_kth(const float* lists, int nl, int st
         int c = 0;
 #pragma unroll
         for (int i = 0; i < 4; ++i) c += __popcll(__builtin_amdgcn_ballot_w64(kv[i] <= mid));
-        if (c >= KP) hi = mid;
+        if (c >= rank) hi = mid;
         else lo = mid + 1;
     }
     return hi;
@@ -120,9 +121,13 @@ __device__ __forceinline__ unsigned union_kth(const float* lists, int nl, int st
 // improving list: entry i of either version still has i + 1 rows of that
 // split at or below it, so counting entries never over-counts rows).  A
 // split that starts late then prunes with what all earlier splits found,
-// not only with the best single split's KP-th key.
+// not only with the best single split's KP-th key.  rank (<= 16, >= k): the
+// union bound is taken at this rank, below KP -- every dropped row then lies
+// above the final shared threshold, which k_refine folds into its
+// certification bound (RefineParams.gtau).
 __device__ __noinline__ void compact_wave(float* lst_d, int* lst_i, int* cnt, float* tau, unsigned* gtq, int qw0,
-                                          int lane, float* pub = nullptr, int splits = 0, int split = 0) {
+                                          int lane, float* pub = nullptr, int splits = 0, int split = 0,
+                                          int rank = KP) {
     uint64_t full = __builtin_amdgcn_ballot_w64(lane < 32 && cnt[qw0 + (lane & 31)] >= CAP);
     while (full) {
         const int qi = __builtin_ctzll(full);
@@ -135,7 +140,10 @@ __device__ __noinline__ void compact_wave(float* lst_d, int* lst_i, int* cnt, fl
             lst_d[q * CAP + lane] = d;
             lst_i[q * CAP + lane] = i;
         }
-        if (lane == KP - 1) {
+        // the list keeps KP entries; the threshold is its rank-th key (rank
+        // = KP unless the union bound is on): published to gtau too, so the
+        // final gtau stays below every split's local threshold (k_refine)
+        if (lane == rank - 1) {
             tau[q] = d;
             if (gtq) atomicMin(gtq + qi, f2ord(d));  // null: no cross-split pruning (k > KP)
         }
@@ -145,8 +153,8 @@ __device__ __noinline__ void compact_wave(float* lst_d, int* lst_i, int* cnt, fl
             if (lane < KP) __hip_atomic_store(qp + split * KP + lane, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const int w0 = split & ~15;
             const int nsp = splits - w0 < 16 ? splits - w0 : 16;
-            const unsigned own = f2ord(__shfl(d, KP - 1, 64));
-            const unsigned v = union_kth(qp + w0 * KP, nsp, KP, own, lane);
+            const unsigned own = f2ord(__shfl(d, rank - 1, 64));
+            const unsigned v = union_kth(qp + w0 * KP, nsp, KP, own, rank, lane);
             if (lane == 0 && v < own) atomicMin(gtq + qi, v);
         }
     }

@@ -19,7 +19,10 @@
 //     (query, corpus split), in the refine's [query tile of 128][split][128][KP]
 //     layout.
 //
-// Not yet measured on hardware: selected only with FX_SCAN_Q32=1.
+// Opt-in (FX_SCAN_Q32=1).  Measured (profiles/r2_sweep_nq.jsonl): at nq = 1 its
+// scan is slower than k_scan_v4's on 10M x 768 bf16 (2.64 vs 2.48 ms) and on
+// 1M x 384 fp32 (0.49 vs 0.32 ms); the search as a whole is faster on the
+// latter through the refine's prefetch (0.79 vs 1.08 ms), so it stays opt-in.
 #include "fx_scan_common.h"
 
 #include <stdlib.h>

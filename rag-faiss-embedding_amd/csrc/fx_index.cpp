@@ -91,7 +91,8 @@ struct FxIndex {
     hipStream_t own_stream = nullptr;
     hipStream_t user_stream = nullptr;
     // search workspace
-    DevBuf qin, qf32, qop, qeps, cand_d, cand_i, dws, iws, flag, fbc_d, fbc_i, stage, gtau, trace, dbgbuf, stamps, pub;
+    DevBuf qin, qf32, qop, qeps, cand_d, cand_i, cand2_d, cand2_i, dws, iws, flag, fbc_d, fbc_i, stage, gtau, trace,
+        dbgbuf, stamps, pub;
     // F32S scan image of an fp32 index (default; FX_F32_SPLIT=0 scans the fp32
     // rows with fp32 MFMA instead): rows [0, split_rows) are current.  L2
     // indexes centre it (FX_CENTER=0: off): image rows fl(y - mu), their
@@ -260,6 +261,13 @@ void plan_scan(const FxIndex* h, int64_t nq, int k, int scan_dt, ScanParams& p) 
 
 // k > KP: approx candidates the refine re-ranks exactly (k_refine_big)
 int big_k1(int k) { return k > KP ? std::max(2 * k, 64) : 0; }
+
+// small batches over many splits: merge the candidate lists 16 splits at a
+// time before the refine (k_reduce_cand; FX_REDUCE_CAND=0 turns it off)
+bool use_reduce(int k, int64_t nq, int splits) {
+    const char* e = getenv("FX_REDUCE_CAND");
+    return k <= KP && nq <= 256 && splits >= 64 && !(e && atoi(e) == 0);
+}
 
 hipError_t ensure_pinned_count(FxIndex* h) {
     if (h->pin_nf) return hipSuccess;
@@ -434,10 +442,23 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
     rp.I = Id;
     rp.n_flag = n_flag;
     rp.flag_list = n_flag + 1;
-    rp.prefetch = sp.q32_tiles > 0 ? 4 : 1;
+    // small batches: one wave per query walks splits * KP candidates (256 splits
+    // at nq = 1); issue 4 chunks of loads at a time (nq = 1: 0.84 -> ~0.3 ms)
+    rp.prefetch = (sp.q32_tiles > 0 || nq <= 256) ? 4 : 1;
     rp.k1 = big_k1(k);
     rp.force_fb = getenv("FX_FORCE_FALLBACK") ? atoi(getenv("FX_FORCE_FALLBACK")) : 0;
     rp.gtau = sp.share ? sp.gtau : nullptr;
+    if (use_reduce(k, nq, cand_splits)) {
+        const size_t nred = (size_t)sp.n_qtiles * ((cand_splits + 15) / 16) * TILE_Q * KP;
+        HIP_TRY(h->cand2_d.ensure(nred * 4));
+        HIP_TRY(h->cand2_i.ensure(nred * 4));
+        int ng = 0;
+        HIP_TRY(launch_reduce_cand(sp.cand_d, sp.cand_i, cand_splits, nq, sp.n_qtiles, (float*)h->cand2_d.p,
+                                   (int*)h->cand2_i.p, &ng, s));
+        rp.cand_d = (const float*)h->cand2_d.p;
+        rp.cand_i = (const int*)h->cand2_i.p;
+        rp.splits = ng;
+    }
     HIP_TRY(launch_refine(h->dtype, h->metric, rp, s));
     if (h->profile) {
         HIP_TRY(hipEventRecord(e2, s));
@@ -522,7 +543,8 @@ std::vector<uint64_t> graph_key(const FxIndex* h, int64_t nq, int q_dtype, int k
             (uint64_t)h->centred,
             (uint64_t)(uintptr_t)h->qin.p, (uint64_t)(uintptr_t)h->qf32.p, (uint64_t)(uintptr_t)h->qop.p,
             (uint64_t)(uintptr_t)h->qeps.p, (uint64_t)(uintptr_t)h->gtau.p, (uint64_t)(uintptr_t)h->cand_d.p,
-            (uint64_t)(uintptr_t)h->cand_i.p, (uint64_t)(uintptr_t)h->dws.p, (uint64_t)(uintptr_t)h->iws.p,
+            (uint64_t)(uintptr_t)h->cand_i.p, (uint64_t)(uintptr_t)h->cand2_d.p, (uint64_t)(uintptr_t)h->cand2_i.p,
+            (uint64_t)(uintptr_t)h->dws.p, (uint64_t)(uintptr_t)h->iws.p,
             (uint64_t)(uintptr_t)h->flag.p, (uint64_t)(uintptr_t)h->fbc_d.p, (uint64_t)(uintptr_t)h->fbc_i.p};
 }
 
@@ -594,7 +616,9 @@ hipError_t graph_build(FxIndex* h, int64_t nq, int q_dtype, int k, bool split) {
     rp.I = (int64_t*)h->iws.p;
     rp.n_flag = n_flag;
     rp.flag_list = n_flag + 1;
-    rp.prefetch = sp.q32_tiles > 0 ? 4 : 1;
+    // small batches: one wave per query walks splits * KP candidates (256 splits
+    // at nq = 1); issue 4 chunks of loads at a time (nq = 1: 0.84 -> ~0.3 ms)
+    rp.prefetch = (sp.q32_tiles > 0 || nq <= 256) ? 4 : 1;
     rp.k1 = big_k1(k);
     rp.force_fb = getenv("FX_FORCE_FALLBACK") ? atoi(getenv("FX_FORCE_FALLBACK")) : 0;
     rp.gtau = sp.share ? sp.gtau : nullptr;
@@ -610,6 +634,14 @@ hipError_t graph_build(FxIndex* h, int64_t nq, int q_dtype, int k, bool split) {
         ce = hipMemsetD32Async((hipDeviceptr_t)sp.gtau, 0xff800000u, (size_t)nq_pad, s);
     if (ce == hipSuccess) ce = launch_scan(scan_dt, h->metric, sp, s);
     if (ce == hipSuccess) ce = hipMemsetAsync(n_flag, 0, 4, s);
+    if (ce == hipSuccess && use_reduce(k, nq, sp.splits)) {  // sized by the preceding do_search
+        int ng = 0;
+        ce = launch_reduce_cand(sp.cand_d, sp.cand_i, sp.splits, nq, sp.n_qtiles, (float*)h->cand2_d.p,
+                                (int*)h->cand2_i.p, &ng, s);
+        rp.cand_d = (const float*)h->cand2_d.p;
+        rp.cand_i = (const int*)h->cand2_i.p;
+        rp.splits = ng;
+    }
     if (ce == hipSuccess) ce = launch_refine(h->dtype, h->metric, rp, s);
     if (ce == hipSuccess)
         ce = launch_exact_fallback(h->dtype, h->metric, h->codes, h->row_bytes, h->kdim, h->ntotal,
@@ -725,7 +757,7 @@ void fx_index_free(FxIndex* h) {
         if (h->max_sq_bits) (void)hipFree(h->max_sq_bits);
         for (DevBuf* b : {&h->qin, &h->qf32, &h->qop, &h->qeps, &h->cand_d, &h->cand_i, &h->dws, &h->iws, &h->flag,
                           &h->fbc_d, &h->fbc_i, &h->stage, &h->gtau, &h->trace, &h->dbgbuf, &h->split, &h->cnorms,
-                          &h->centre, &h->mu_part, &h->qxn2, &h->stamps, &h->pub})
+                          &h->centre, &h->mu_part, &h->qxn2, &h->stamps, &h->pub, &h->cand2_d, &h->cand2_i})
             b->release();
         graph_release(h);
         if (h->ghq) (void)hipHostFree(h->ghq);

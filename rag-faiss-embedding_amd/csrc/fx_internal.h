@@ -136,6 +136,10 @@ hipError_t launch_scan_w(int st_dt, int metric, const ScanParams& p, hipStream_t
 bool scan_w_supported(int st_dt, int row_bytes);
 int scan_w_queries();
 hipError_t launch_refine(int st_dt, int metric, const RefineParams& p, hipStream_t s);
+// small batches: merge each 16 splits' candidate lists of a query into their
+// top KP (k_reduce_cand); *ngroups = ceil(splits / 16) lists per query after
+hipError_t launch_reduce_cand(const float* cd, const int* ci, int splits, int64_t nq, int n_qtiles, float* od,
+                              int* oi, int* ngroups, hipStream_t s);
 // both fallback launches, always enqueued; they read the flagged count at
 // n_flag[0] (list at n_flag + 1) and do nothing when it is 0
 hipError_t launch_exact_fallback(int st_dt, int metric, const char* codes, int row_bytes, int kdim,

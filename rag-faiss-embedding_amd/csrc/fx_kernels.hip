@@ -691,6 +691,62 @@ __device__ __forceinline__ void refine_take(float d, int i, float& bd, int& bi, 
     ti = __shfl(bi, KP - 1, 64);
 }
 
+// Small batches scan with many corpus splits (1,024 at nq = 1 on 10M rows),
+// which leaves one refine wave per query walking splits * KP candidates.
+// This pre-pass merges every G splits' lists of a query into their top KP
+// (one wave per (query, group of G splits), all loads issued first), written
+// in the same [qtile][group][128][KP] layout; the refine then reads
+// ceil(splits / G) lists.  The union of the groups' top KP holds the global
+// top KP under the (key, id) order, so the refine's selection, its KP-th key
+// and its "at least KP valid candidates" test are unchanged.
+template <int G>
+__global__ __launch_bounds__(256) void k_reduce_cand(const float* __restrict__ cd, const int* __restrict__ ci,
+                                                     int splits, int64_t nq, int ngroups, float* __restrict__ od,
+                                                     int* __restrict__ oi) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t q = w / ngroups;
+    const int g = (int)(w - q * ngroups);
+    if (q >= nq) return;
+    const int qtile = (int)(q / TILE_Q), qq = (int)(q % TILE_Q);
+    const int s0 = g * G, ns = min(G, splits - s0);
+    constexpr int NL = G * KP / 64;  // loads per lane
+    float dv[NL];
+    int iv[NL];
+#pragma unroll
+    for (int u = 0; u < NL; ++u) {
+        const int c = u * 64 + lane, s = c / KP, j = c - s * KP;
+        dv[u] = FX_INF;
+        iv[u] = INT_MAX;
+        if (s < ns) {
+            const int64_t off = (((int64_t)qtile * splits + s0 + s) * TILE_Q + qq) * KP + j;
+            const int ii = ci[off];
+            const float dd = cd[off];
+            if (ii >= 0) { dv[u] = dd; iv[u] = ii; }
+        }
+    }
+    float bd = FX_INF, td = FX_INF;
+    int bi = INT_MAX, ti = INT_MAX, nvalid = 0;
+#pragma unroll
+    for (int u = 0; u < NL; ++u) refine_take(dv[u], iv[u], bd, bi, td, ti, nvalid, lane);
+    if (lane < KP) {
+        const int64_t o = (((int64_t)qtile * ngroups + g) * TILE_Q + qq) * KP + lane;
+        od[o] = bd;
+        oi[o] = bi == INT_MAX ? -1 : bi;
+    }
+}
+
+hipError_t launch_reduce_cand(const float* cd, const int* ci, int splits, int64_t nq, int n_qtiles, float* od,
+                              int* oi, int* ngroups, hipStream_t s) {
+    constexpr int G = 16;
+    *ngroups = (splits + G - 1) / G;
+    (void)n_qtiles;
+    const int64_t waves = nq * (int64_t)*ngroups;
+    hipLaunchKernelGGL((k_reduce_cand<G>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, cd, ci, splits, nq,
+                       *ngroups, od, oi);
+    return hipGetLastError();
+}
+
 // PF = chunks of 64 candidates whose loads are issued together in phase 1
 // (PF = 4 for the small-batch scan's many splits: one wave per query is
 // latency-bound on one dependent load per chunk otherwise)

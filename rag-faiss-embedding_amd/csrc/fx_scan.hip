@@ -223,7 +223,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
     // ABL & 64: per-wave cycle sums {stage wait + barrier, half 0, mid-stage
     // LDS wait, half 1, epilogue, stages, slow-path tiles, slow-path cycles,
     // compaction calls, compaction cycles, group pushes, -}
-    uint64_t stq[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t stq[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // [11]: slow path up to the first compaction
     uint64_t s_end = 0;
     for (int t = 0; t < ntiles; ++t) {
         float tr[N];
@@ -432,6 +432,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                     });
                 }
             });
+            if constexpr (ABL & 64) stq[11] += __builtin_amdgcn_s_memtime() - s_sl;
             while (__builtin_amdgcn_ballot_w64(ovf)) {
                 uint64_t s_cp = 0;
                 if constexpr (ABL & 64) s_cp = __builtin_amdgcn_s_memtime();

@@ -24,3 +24,4 @@ print(f"  slow-path tiles {np.mean(a[:, 6] / tiles):.3f} of tiles, {np.mean(a[:,
       f"{100 * a[:, 7].sum() / tot.sum():.1f} % of wave time")
 print(f"  compactions {np.mean(a[:, 8] / tiles):.4f} per tile, {np.mean(a[:, 9] / np.maximum(a[:, 8], 1)):.0f} cyc each, "
       f"{100 * a[:, 9].sum() / tot.sum():.1f} % of wave time; group pushes {np.mean(a[:, 10] / np.maximum(a[:, 6], 1)):.2f} per slow tile")
+print(f"  slow path before any compaction: {np.mean(a[:, 11] / np.maximum(a[:, 6], 1)):.0f} cyc per slow tile")

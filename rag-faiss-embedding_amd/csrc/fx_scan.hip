@@ -42,6 +42,9 @@
 #ifndef FX_V4_LATEMIN
 #define FX_V4_LATEMIN 1   // 1: group minima after the tile; 0: beside its last MFMAs (no gain measured)
 #endif
+#ifndef FX_V4_DMAPOS
+#define FX_V4_DMAPOS 0    // MFMA pairs after which a stage's corpus pieces issue: 0 (4,6 | 4,5), 1 (1,5 | 1,5),
+#endif                    // 2 (2,6 | 2,6), 3 (3,7 | 3,7)
 #ifndef FX_V4_ATOMPUSH
 #define FX_V4_ATOMPUSH 0  // 1: push_group (branchy, one atomic per lane) instead of push_lean
 #endif
@@ -291,8 +294,10 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                         if constexpr (jp == 0) piece(std::integral_constant<int, 4>{}, JP{}, NXT{}, c4, tnext);
                     }
                 } else {
-                    if constexpr (m == 4) piece(std::integral_constant<int, 0>{}, JP{}, NXT{}, c4, tnext);
-                    if constexpr (m == 6) piece(std::integral_constant<int, 1>{}, JP{}, NXT{}, c4, tnext);
+                    constexpr int P0 = FX_V4_DMAPOS == 0 ? 4 : FX_V4_DMAPOS;
+                    constexpr int P1 = FX_V4_DMAPOS == 0 ? 6 : FX_V4_DMAPOS + 4;
+                    if constexpr (m == P0) piece(std::integral_constant<int, 0>{}, JP{}, NXT{}, c4, tnext);
+                    if constexpr (m == P1) piece(std::integral_constant<int, 1>{}, JP{}, NXT{}, c4, tnext);
                 }
             });
             if constexpr (HI) {  // hi * x_lo (>= 14 MFMAs after each accumulator's previous write)
@@ -353,9 +358,12 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                     ds_rd128<(2 * m + 1) * 2048>(X[2 * m + 1], rd_next);
                 }
                 if constexpr (!(ABL & 128)) {
-                    if constexpr (m == 4) piece(std::integral_constant<int, 2>{}, JP{}, NXT{}, c4, tnext);
-                    if constexpr (m == 5) piece(std::integral_constant<int, 3>{}, JP{}, NXT{}, c4, tnext);
-                    if constexpr (m == 6 && jp == 0) piece(std::integral_constant<int, 4>{}, JP{}, NXT{}, c4, tnext);
+                    constexpr int P2 = FX_V4_DMAPOS == 0 ? 4 : FX_V4_DMAPOS;
+                    constexpr int P3 = FX_V4_DMAPOS == 0 ? 5 : FX_V4_DMAPOS + 4;
+                    constexpr int P4 = FX_V4_DMAPOS == 0 ? 6 : (FX_V4_DMAPOS + 5) % 8;
+                    if constexpr (m == P2) piece(std::integral_constant<int, 2>{}, JP{}, NXT{}, c4, tnext);
+                    if constexpr (m == P3) piece(std::integral_constant<int, 3>{}, JP{}, NXT{}, c4, tnext);
+                    if constexpr (m == P4 && jp == 0) piece(std::integral_constant<int, 4>{}, JP{}, NXT{}, c4, tnext);
                 }
             });
             if constexpr (HI) {

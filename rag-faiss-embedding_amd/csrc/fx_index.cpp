@@ -246,6 +246,8 @@ void plan_scan(const FxIndex* h, int64_t nq, int k, int scan_dt, ScanParams& p) 
             if (eff > best_eff + 1e-9) { best_eff = eff; best = sx; }
             if (eff > 0.985 && live >= 128) break;
         }
+        // FX_SCAN_SX: splits per XCD, for placement A/B runs only
+        if (const char* sx_env = getenv("FX_SCAN_SX"); sx_env && *sx_env) best = std::max(1, std::min(max_sx, atoi(sx_env)));
         if (k > KP) best = std::max(best, std::min(max_sx, ((k + 3) / 4 + 7) / 8));
         p.sx = best;
         p.splits = 8 * best;

@@ -142,7 +142,22 @@ __global__ __launch_bounds__(256) void k_convert_rows(const void* __restrict__ x
 // chunk load of those rows before converting any (up to CPL 16-B chunks in
 // flight per lane), and reduces the R row norms together.  Chunks partly or
 // wholly past d (row padding) take the element path.
-template <int XDT, int SDT, bool NORM>
+// streamed-once operands of add(): NT = nontemporal loads / stores (the rows
+// are read once and the codes are not re-read by this launch)
+typedef unsigned cv_u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned cv_u32x2 __attribute__((ext_vector_type(2)));
+template <bool NT, typename V>
+__device__ __forceinline__ V cv_load(const void* p) {
+    if constexpr (NT) return __builtin_nontemporal_load((const V*)p);
+    else return *(const V*)p;
+}
+template <bool NT>
+__device__ __forceinline__ void cv_store16(void* p, cv_u32x4 v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, (cv_u32x4*)p);
+    else *(cv_u32x4*)p = v;
+}
+
+template <int XDT, int SDT, bool NORM, bool NT>
 __global__ __launch_bounds__(256) void k_convert_rows_t(const void* __restrict__ x, int64_t n, int d,
                                                         void* __restrict__ codes, int kdim, float* __restrict__ norms,
                                                         unsigned* __restrict__ max_sq_bits, int R) {
@@ -171,23 +186,25 @@ __global__ __launch_bounds__(256) void k_convert_rows_t(const void* __restrict__
             if (c < tot && r < n && e0 + E <= d) {
                 const char* src = (const char*)x + ((r * d + e0) * (XDT == F32 ? 4 : 2));
                 if constexpr (XDT == F32) {
-                    const float4 a = *(const float4*)src;
-                    v[k][0] = a.x; v[k][1] = a.y; v[k][2] = a.z; v[k][3] = a.w;
+                    const cv_u32x4 a = cv_load<NT, cv_u32x4>(src);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) v[k][j] = __uint_as_float(a[j]);
                     if constexpr (E == 8) {
-                        const float4 b = *(const float4*)(src + 16);
-                        v[k][4] = b.x; v[k][5] = b.y; v[k][6] = b.z; v[k][7] = b.w;
+                        const cv_u32x4 b = cv_load<NT, cv_u32x4>(src + 16);
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) v[k][4 + j] = __uint_as_float(b[j]);
                     }
                 } else if constexpr (E == 8) {
-                    const uint4 a = *(const uint4*)src;
-                    const uint32_t w[4] = {a.x, a.y, a.z, a.w};
+                    const cv_u32x4 a = cv_load<NT, cv_u32x4>(src);
+                    const uint32_t w[4] = {a[0], a[1], a[2], a[3]};
 #pragma unroll
                     for (int j = 0; j < 8; ++j) {
                         const uint16_t hv = (uint16_t)(w[j >> 1] >> (16 * (j & 1)));
                         v[k][j] = XDT == BF16 ? bf2f(hv) : h2f(hv);
                     }
                 } else {
-                    const uint2 a = *(const uint2*)src;
-                    const uint32_t w[2] = {a.x, a.y};
+                    const cv_u32x2 a = cv_load<NT, cv_u32x2>(src);
+                    const uint32_t w[2] = {a[0], a[1]};
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const uint16_t hv = (uint16_t)(w[j >> 1] >> (16 * (j & 1)));
@@ -241,7 +258,8 @@ __global__ __launch_bounds__(256) void k_convert_rows_t(const void* __restrict__
                 o.x = v[k][0] * sc; o.y = v[k][1] * sc; o.z = v[k][2] * sc; o.w = v[k][3] * sc;
                 part = fmaf(o.x, o.x, part); part = fmaf(o.y, o.y, part);
                 part = fmaf(o.z, o.z, part); part = fmaf(o.w, o.w, part);
-                *(float4*)out = o;
+                cv_store16<NT>(out, cv_u32x4{__float_as_uint(o.x), __float_as_uint(o.y), __float_as_uint(o.z),
+                                             __float_as_uint(o.w)});
             } else {
                 uint32_t w[4];
 #pragma unroll
@@ -253,7 +271,7 @@ __global__ __launch_bounds__(256) void k_convert_rows_t(const void* __restrict__
                     part = fmaf(s1, s1, part);
                     w[j >> 1] = (uint32_t)h0 | ((uint32_t)h1 << 16);
                 }
-                *(uint4*)out = make_uint4(w[0], w[1], w[2], w[3]);
+                cv_store16<NT>(out, cv_u32x4{w[0], w[1], w[2], w[3]});
             }
 #pragma unroll
             for (int q = 0; q < RMAX; ++q) sq[q] += rr == q ? part : 0.0f;
@@ -1150,20 +1168,29 @@ hipError_t launch_convert_rows(const void* x, int x_dt, int64_t n, int d, void* 
     while (R < 4 && (R * nchunk) % 64 != 0) R *= 2;
     if (vec && R * nchunk <= 256 && !getenv("FX_CONVERT_V1")) {
         const unsigned grid = grid_for((n + R - 1) / R, 4, 65536);
-#define FX_CONV(XD, SD)                                                                                           \
-        if (x_dt == XD && st_dt == SD) {                                                                         \
+        // FX_CONVERT_NT=1: nontemporal loads / stores instead of cached ones
+        static const bool nt = getenv("FX_CONVERT_NT") && atoi(getenv("FX_CONVERT_NT")) == 1;
+#define FX_CONV_NT(XD, SD, NT)                                                                                    \
             if (normalize)                                                                                       \
-                hipLaunchKernelGGL((k_convert_rows_t<XD, SD, true>), dim3(grid), dim3(256), 0, s, x, n, d,       \
+                hipLaunchKernelGGL((k_convert_rows_t<XD, SD, true, NT>), dim3(grid), dim3(256), 0, s, x, n, d,   \
                                    codes_row0, kdim, norms_row0, max_sq_bits, R);                               \
             else                                                                                                 \
-                hipLaunchKernelGGL((k_convert_rows_t<XD, SD, false>), dim3(grid), dim3(256), 0, s, x, n, d,      \
-                                   codes_row0, kdim, norms_row0, max_sq_bits, R);                               \
+                hipLaunchKernelGGL((k_convert_rows_t<XD, SD, false, NT>), dim3(grid), dim3(256), 0, s, x, n, d,  \
+                                   codes_row0, kdim, norms_row0, max_sq_bits, R);
+#define FX_CONV(XD, SD)                                                                                           \
+        if (x_dt == XD && st_dt == SD) {                                                                         \
+            if (nt) {                                                                                            \
+                FX_CONV_NT(XD, SD, true)                                                                         \
+            } else {                                                                                             \
+                FX_CONV_NT(XD, SD, false)                                                                        \
+            }                                                                                                    \
             return hipGetLastError();                                                                            \
         }
         FX_CONV(F32, F32) FX_CONV(F32, BF16) FX_CONV(F32, F16)
         FX_CONV(BF16, F32) FX_CONV(BF16, BF16) FX_CONV(BF16, F16)
         FX_CONV(F16, F32) FX_CONV(F16, BF16) FX_CONV(F16, F16)
 #undef FX_CONV
+#undef FX_CONV_NT
     }
     hipLaunchKernelGGL(k_convert_rows, dim3(grid_for(n, 4, 65536)), dim3(256), 0, s, x, x_dt, n, d, codes_row0,
                        st_dt, kdim, norms_row0, max_sq_bits, normalize, vec);

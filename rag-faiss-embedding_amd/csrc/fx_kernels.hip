@@ -1168,8 +1168,9 @@ hipError_t launch_convert_rows(const void* x, int x_dt, int64_t n, int d, void* 
     while (R < 4 && (R * nchunk) % 64 != 0) R *= 2;
     if (vec && R * nchunk <= 256 && !getenv("FX_CONVERT_V1")) {
         const unsigned grid = grid_for((n + R - 1) / R, 4, 65536);
-        // FX_CONVERT_NT=1: nontemporal loads / stores instead of cached ones
-        static const bool nt = getenv("FX_CONVERT_NT") && atoi(getenv("FX_CONVERT_NT")) == 1;
+        // nontemporal loads / stores by default (1M x 768 bf16: 0.900 -> 0.882 ms,
+        // same box); FX_CONVERT_NT=0: cached ones
+        static const bool nt = !(getenv("FX_CONVERT_NT") && atoi(getenv("FX_CONVERT_NT")) == 0);
 #define FX_CONV_NT(XD, SD, NT)                                                                                    \
             if (normalize)                                                                                       \
                 hipLaunchKernelGGL((k_convert_rows_t<XD, SD, true, NT>), dim3(grid), dim3(256), 0, s, x, n, d,   \

@@ -157,13 +157,13 @@ __device__ __forceinline__ void cv_store16(void* p, cv_u32x4 v) {
     else *(cv_u32x4*)p = v;
 }
 
-template <int XDT, int SDT, bool NORM, bool NT>
+template <int XDT, int SDT, bool NORM, bool NT, int CPL>
 __global__ __launch_bounds__(256) void k_convert_rows_t(const void* __restrict__ x, int64_t n, int d,
                                                         void* __restrict__ codes, int kdim, float* __restrict__ norms,
                                                         unsigned* __restrict__ max_sq_bits, int R) {
     constexpr int E = SDT == F32 ? 4 : 8;    // values per 16-B output chunk
-    constexpr int CPL = 4;                   // chunks per lane per wave iteration
-    constexpr int RMAX = 4;
+    // CPL: chunks per lane per wave iteration (all loaded before any store)
+    constexpr int RMAX = CPL;
     __shared__ unsigned bmax;
     if (threadIdx.x == 0) bmax = 0u;
     __syncthreads();
@@ -222,7 +222,7 @@ __global__ __launch_bounds__(256) void k_convert_rows_t(const void* __restrict__
 #pragma unroll
         for (int q = 0; q < RMAX; ++q) scale[q] = 1.0f;
         if constexpr (NORM) {
-            double sr[RMAX] = {0.0, 0.0, 0.0, 0.0};
+            double sr[RMAX] = {};
 #pragma unroll
             for (int k = 0; k < CPL; ++k) {
                 const int rr = (lane + 64 * k) / nchunk;
@@ -241,7 +241,7 @@ __global__ __launch_bounds__(256) void k_convert_rows_t(const void* __restrict__
             }
         }
         // convert, store, |y|^2 of the stored values
-        float sq[RMAX] = {0.f, 0.f, 0.f, 0.f};
+        float sq[RMAX] = {};
 #pragma unroll
         for (int k = 0; k < CPL; ++k) {
             const int c = lane + 64 * k;
@@ -1166,24 +1166,31 @@ hipError_t launch_convert_rows(const void* x, int x_dt, int64_t n, int d, void* 
     const int nchunk = kdim / (st_dt == F32 ? 4 : 8);
     int R = 1;
     while (R < 4 && (R * nchunk) % 64 != 0) R *= 2;
-    if (vec && R * nchunk <= 256 && !getenv("FX_CONVERT_V1")) {
+    // FX_CONVERT_WIDE=1: twice the rows per wave iteration (up to 8 chunks in
+    // flight per lane)
+    static const bool wide = getenv("FX_CONVERT_WIDE") && atoi(getenv("FX_CONVERT_WIDE")) == 1;
+    const int cpl = wide && (R * nchunk) % 64 == 0 && 2 * R * nchunk <= 512 ? 8 : 4;
+    if (cpl == 8) R *= 2;
+    if (vec && R * nchunk <= 64 * cpl && !getenv("FX_CONVERT_V1")) {
         const unsigned grid = grid_for((n + R - 1) / R, 4, 65536);
         // nontemporal loads / stores by default (1M x 768 bf16: 0.900 -> 0.882 ms,
         // same box); FX_CONVERT_NT=0: cached ones
         static const bool nt = !(getenv("FX_CONVERT_NT") && atoi(getenv("FX_CONVERT_NT")) == 0);
-#define FX_CONV_NT(XD, SD, NT)                                                                                    \
+#define FX_CONV_NT(XD, SD, NT, C)                                                                                 \
             if (normalize)                                                                                       \
-                hipLaunchKernelGGL((k_convert_rows_t<XD, SD, true, NT>), dim3(grid), dim3(256), 0, s, x, n, d,   \
-                                   codes_row0, kdim, norms_row0, max_sq_bits, R);                               \
+                hipLaunchKernelGGL((k_convert_rows_t<XD, SD, true, NT, C>), dim3(grid), dim3(256), 0, s, x, n,   \
+                                   d, codes_row0, kdim, norms_row0, max_sq_bits, R);                            \
             else                                                                                                 \
-                hipLaunchKernelGGL((k_convert_rows_t<XD, SD, false, NT>), dim3(grid), dim3(256), 0, s, x, n, d,  \
-                                   codes_row0, kdim, norms_row0, max_sq_bits, R);
+                hipLaunchKernelGGL((k_convert_rows_t<XD, SD, false, NT, C>), dim3(grid), dim3(256), 0, s, x, n,  \
+                                   d, codes_row0, kdim, norms_row0, max_sq_bits, R);
 #define FX_CONV(XD, SD)                                                                                           \
         if (x_dt == XD && st_dt == SD) {                                                                         \
-            if (nt) {                                                                                            \
-                FX_CONV_NT(XD, SD, true)                                                                         \
+            if (cpl == 8) {                                                                                      \
+                FX_CONV_NT(XD, SD, true, 8)                                                                      \
+            } else if (nt) {                                                                                     \
+                FX_CONV_NT(XD, SD, true, 4)                                                                      \
             } else {                                                                                             \
-                FX_CONV_NT(XD, SD, false)                                                                        \
+                FX_CONV_NT(XD, SD, false, 4)                                                                     \
             }                                                                                                    \
             return hipGetLastError();                                                                            \
         }

@@ -1172,7 +1172,11 @@ hipError_t launch_convert_rows(const void* x, int x_dt, int64_t n, int d, void* 
     const int cpl = wide && (R * nchunk) % 64 == 0 && 2 * R * nchunk <= 512 ? 8 : 4;
     if (cpl == 8) R *= 2;
     if (vec && R * nchunk <= 64 * cpl && !getenv("FX_CONVERT_V1")) {
-        const unsigned grid = grid_for((n + R - 1) / R, 4, 65536);
+        // grid-stride over row groups with a bounded grid: one atomicMax per
+        // workgroup lands on ONE address (max_sq_bits), so 65536 workgroups
+        // serialised there; FX_CONVERT_GRID overrides the cap (A/B runs)
+        static const int gcap = getenv("FX_CONVERT_GRID") ? std::max(1, atoi(getenv("FX_CONVERT_GRID"))) : 65536;
+        const unsigned grid = grid_for((n + R - 1) / R, 4, gcap);
         // nontemporal loads / stores by default (1M x 768 bf16: 0.900 -> 0.882 ms,
         // same box); FX_CONVERT_NT=0: cached ones
         static const bool nt = !(getenv("FX_CONVERT_NT") && atoi(getenv("FX_CONVERT_NT")) == 0);

@@ -1151,6 +1151,14 @@ __global__ __launch_bounds__(256) void k_to_f32(const char* __restrict__ codes, 
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
+// Row kernels (add() conversion, split image) end each workgroup with one
+// atomicMax on a single word (the max row norm): at 65,536 workgroups those
+// serialised and set the kernel time (1M x 768 bf16: 0.86 ms whatever the
+// bytes); a grid-stride launch of 4,096 workgroups (16 per CU) moves the same
+// chunk in 0.574 ms = 5.36 TB/s, above a torch device copy on the same box
+// (profiles/r2/add_grid_ab.txt)
+constexpr int ROWS_GRID_CAP = 4096;
+
 static inline int grid_for(int64_t items, int per_block, int cap) {
     int64_t g = (items + per_block - 1) / per_block;
     if (g < 1) g = 1;
@@ -1172,10 +1180,10 @@ hipError_t launch_convert_rows(const void* x, int x_dt, int64_t n, int d, void* 
     const int cpl = wide && (R * nchunk) % 64 == 0 && 2 * R * nchunk <= 512 ? 8 : 4;
     if (cpl == 8) R *= 2;
     if (vec && R * nchunk <= 64 * cpl && !getenv("FX_CONVERT_V1")) {
-        // grid-stride over row groups with a bounded grid: one atomicMax per
-        // workgroup lands on ONE address (max_sq_bits), so 65536 workgroups
-        // serialised there; FX_CONVERT_GRID overrides the cap (A/B runs)
-        static const int gcap = getenv("FX_CONVERT_GRID") ? std::max(1, atoi(getenv("FX_CONVERT_GRID"))) : 65536;
+        // grid-stride over row groups with a bounded grid (ROWS_GRID_CAP);
+        // FX_CONVERT_GRID overrides the cap (A/B runs)
+        static const int gcap =
+            getenv("FX_CONVERT_GRID") ? std::max(1, atoi(getenv("FX_CONVERT_GRID"))) : ROWS_GRID_CAP;
         const unsigned grid = grid_for((n + R - 1) / R, 4, gcap);
         // nontemporal loads / stores by default (1M x 768 bf16: 0.900 -> 0.882 ms,
         // same box); FX_CONVERT_NT=0: cached ones
@@ -1204,7 +1212,7 @@ hipError_t launch_convert_rows(const void* x, int x_dt, int64_t n, int d, void* 
 #undef FX_CONV
 #undef FX_CONV_NT
     }
-    hipLaunchKernelGGL(k_convert_rows, dim3(grid_for(n, 4, 65536)), dim3(256), 0, s, x, x_dt, n, d, codes_row0,
+    hipLaunchKernelGGL(k_convert_rows, dim3(grid_for(n, 4, ROWS_GRID_CAP)), dim3(256), 0, s, x, x_dt, n, d, codes_row0,
                        st_dt, kdim, norms_row0, max_sq_bits, normalize, vec);
     return hipGetLastError();
 }
@@ -1212,7 +1220,7 @@ hipError_t launch_convert_rows(const void* x, int x_dt, int64_t n, int d, void* 
 hipError_t launch_split_rows(const float* codes, int kdim, int64_t r0, int64_t r1, const float* mu, void* split,
                              float* cnorms, unsigned* cmax_bits, hipStream_t s) {
     if (r1 <= r0) return hipSuccess;
-    hipLaunchKernelGGL(k_split_rows, dim3(grid_for(r1 - r0, 4, 65536)), dim3(256), 0, s, codes, kdim, r0, r1, mu,
+    hipLaunchKernelGGL(k_split_rows, dim3(grid_for(r1 - r0, 4, ROWS_GRID_CAP)), dim3(256), 0, s, codes, kdim, r0, r1, mu,
                        (uint16_t*)split, cnorms, cmax_bits);
     return hipGetLastError();
 }

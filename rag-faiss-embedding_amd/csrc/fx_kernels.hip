@@ -5,7 +5,8 @@
 //
 //   k_convert_rows   add(): dtype conversion into the HBM-resident, 128-B
 //                    row-aligned code matrix + |y|^2 per row (+ opt-in row
-//                    L2 normalisation) -- one wave per row, HBM-bound.
+//                    L2 normalisation) -- R rows per wave, grid-stride over
+//                    4,096 workgroups, nontemporal, HBM-bound.
 //   k_prep_queries   search(): fp32 copy of the queries for the exact refine,
 //                    storage-dtype operand for the MFMA scan, per-query
 //                    certification margin.

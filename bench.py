@@ -255,11 +255,9 @@ def main():
         roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(gbs / HBM_PEAK_GBS, 4)}
     # the committed PMC pass measured the default scan: no traffic figure for an opt-in variant
-    variant = (os.environ.get("FX_SCAN_Q32", "0") != "0" or os.environ.get("FX_F32_SPLIT", "1") == "0"
-               or os.environ.get("FX_SCAN_LINE", "1") == "0")
+    variant = os.environ.get("FX_F32_SPLIT", "1") == "0"
     roof["traffic"] = None if variant else read_pmc_traffic(args.config, n_local, nq)
-    scan_kernel = "k_scan_q32" if os.environ.get("FX_SCAN_Q32") == "1" and nq <= 32 else "k_scan_v4"
-    roof["kernel"] = scan_kernel + \
+    roof["kernel"] = "k_scan_v4" + \
         (" F32S (fp32 as 3 bf16 MFMA products)" if split else "") + " (fused MFMA distance GEMM + top-k select)"
     roof["kernel_ms_avg"] = round(scan_avg_ms, 4)
     roof["launches"] = launches

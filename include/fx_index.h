@@ -81,8 +81,18 @@ int fx_index_set_normalize(FxIndex* index, int on);
 /* Run the index's kernels on `stream` (a hipStream_t; NULL = the index's own
  * stream, which is a blocking stream and therefore ordered with work on the
  * legacy null stream).  Lets a caller order index work after its own
- * producers. */
+ * producers.  Switching streams keeps the index's calls in order: the new
+ * stream waits (on the device, no host sync) for the work already enqueued on
+ * the previous one. */
 int fx_index_set_stream(FxIndex* index, void* stream);
+/* Per-index tuning / diagnostic option (name -> integer value).  Initial
+ * values come from the FX_* environment variables, read once at index
+ * creation; nothing on the search path reads the environment.  Names:
+ * "search_graph" (replay small host searches as one hipGraph), "force_fallback"
+ * (test hook: every query through the exact fallback), "scan_place",
+ * "scan_sx", "reduce_cand", "f32_split", "centre", "scan_pub", "prune_rank",
+ * "scan_dbg" (see DESIGN.md 3).  Unknown name: FX_E_ARG. */
+int fx_index_set_option(FxIndex* index, const char* name, int64_t value);
 /* Global id of local row 0 (row-sharded multi-GPU: shard offset). */
 int fx_index_set_id_offset(FxIndex* index, int64_t offset);
 

@@ -48,6 +48,7 @@ SIGNATURES = {
     "fx_index_set_normalize": (_i, [_vp, _i]),
     "fx_index_set_stream": (_i, [_vp, _vp]),
     "fx_index_set_id_offset": (_i, [_vp, _i64]),
+    "fx_index_set_option": (_i, [_vp, ctypes.c_char_p, _i64]),
     "fx_index_dim": (_i, [_vp, ctypes.POINTER(_i)]),
     "fx_index_ntotal": (_i, [_vp, ctypes.POINTER(_i64)]),
     "fx_index_storage_dtype": (_i, [_vp, ctypes.POINTER(_i)]),

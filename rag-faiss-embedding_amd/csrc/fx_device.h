@@ -116,8 +116,7 @@ __device__ __forceinline__ void glds16(const void* gsrc, char* lds_uniform) {
     __builtin_amdgcn_global_load_lds(gsrc, (__attribute__((address_space(3))) void*)lds_uniform, 16, 0, 0);
 }
 
-// blockIdx -> (query tile, corpus split) over `ntl` query tiles (the scan's
-// own tile: 128 queries for k_scan_v4, scan_w_queries() for k_scan_w).
+// blockIdx -> (query tile, corpus split) over `ntl` query tiles of 128.
 // Placement only changes speed, never results; both forms rely on the
 // observed round-robin dispatch of blocks over the 8 XCDs (b, b + 8, ... share
 // one XCD).

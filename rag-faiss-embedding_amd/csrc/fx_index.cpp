@@ -79,6 +79,64 @@ struct DevBuf {
 
 inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
+// Per-index tuning and diagnostic options.  Initial values come from the
+// FX_* environment variables, read ONCE when the index is created (never on
+// the search path); fx_index_set_option changes them afterwards.
+struct Options {
+    int search_graph = 0;    // FX_SEARCH_GRAPH: replay small host searches as one hipGraph
+    int force_fallback = 0;  // FX_FORCE_FALLBACK: flag every query (test hook of the exact fallback)
+    int place = -1;          // FX_SCAN_PLACE: scan block placement (-1 automatic, 0, 1)
+    int sx = 0;              // FX_SCAN_SX: corpus splits per XCD under placement 1 (0 automatic)
+    int reduce_cand = 1;     // FX_REDUCE_CAND: merge 16 splits' lists before the refine (small nq)
+    int f32_split = 1;       // FX_F32_SPLIT: fp32 indexes scan their split-bf16 image
+    int centre = 1;          // FX_CENTER: L2 scan images are centred on a row sample's mean
+    int pub = 1;             // FX_SCAN_PUB: union threshold over published per-split lists
+    int prune_rank = 0;      // FX_PRUNE_RANK: rank of the shared threshold (0: max(2k, 16))
+    int scan_dbg = 0;        // FX_SCAN_DBG: ablation switches of -DFX_ABLATION builds / key dump (32)
+    int graph_verbose = 0;   // FX_SEARCH_GRAPH_VERBOSE
+    std::string trace, stamps, cand, keys;  // FX_SCAN_TRACE / _STAMPS / _CAND / _KEYS dump paths
+
+    void from_env() {
+        auto num = [](const char* name, int& v) {
+            if (const char* e = getenv(name); e && *e) v = atoi(e);
+        };
+        auto str = [](const char* name, std::string& v) {
+            if (const char* e = getenv(name); e && *e) v = e;
+        };
+        num("FX_SEARCH_GRAPH", search_graph);
+        num("FX_FORCE_FALLBACK", force_fallback);
+        num("FX_SCAN_PLACE", place);
+        num("FX_SCAN_SX", sx);
+        num("FX_REDUCE_CAND", reduce_cand);
+        num("FX_F32_SPLIT", f32_split);
+        num("FX_CENTER", centre);
+        num("FX_SCAN_PUB", pub);
+        num("FX_PRUNE_RANK", prune_rank);
+        num("FX_SCAN_DBG", scan_dbg);
+        num("FX_SEARCH_GRAPH_VERBOSE", graph_verbose);
+        str("FX_SCAN_TRACE", trace);
+        str("FX_SCAN_STAMPS", stamps);
+        str("FX_SCAN_CAND", cand);
+        str("FX_SCAN_KEYS", keys);
+    }
+    int* find(const char* name) {
+        static const char* names[] = {"search_graph", "force_fallback", "scan_place", "scan_sx", "reduce_cand",
+                                      "f32_split", "centre", "scan_pub", "prune_rank", "scan_dbg"};
+        int* slots[] = {&search_graph, &force_fallback, &place, &sx, &reduce_cand,
+                        &f32_split, &centre, &pub, &prune_rank, &scan_dbg};
+        for (int i = 0; i < (int)(sizeof(names) / sizeof(names[0])); ++i)
+            if (strcmp(name, names[i]) == 0) return slots[i];
+        return nullptr;
+    }
+};
+
+// scan image of the index (what the MFMA scan streams, and its row constants)
+enum ImageKind {
+    IMG_NONE = 0,  // the stored rows with srcC = |y|^2 (IP: no row constant)
+    IMG_F32S = 1,  // fp32 index: [hi | lo] bf16 planes of fl(y - mu), srcC = |y - mu|^2
+    IMG_C16 = 2,   // bf16 / fp16 L2 index: the stored rows, srcC = |y - mu|^2 (the query operand is x - mu)
+};
+
 }  // namespace
 
 struct FxIndex {
@@ -87,25 +145,31 @@ struct FxIndex {
     int64_t ntotal = 0, cap_rows = 0, id_offset = 0;
     char* codes = nullptr;
     float* norms = nullptr;
-    unsigned* max_sq_bits = nullptr;  // device
+    // device words: [0] max |y|^2 of the stored rows, [1] max srcC of the scan
+    // image (F32S / C16), as float bits (non-negative floats order as uints)
+    unsigned* max_sq_bits = nullptr;
     hipStream_t own_stream = nullptr;
     hipStream_t user_stream = nullptr;
+    hipEvent_t switch_ev = nullptr;  // orders the work of a stream the index leaves before the next one's
+    Options opt;
     // search workspace
-    DevBuf qin, qf32, qop, qeps, cand_d, cand_i, cand2_d, cand2_i, dws, iws, flag, fbc_d, fbc_i, stage, gtau, trace,
-        dbgbuf, stamps, pub;
-    // F32S scan image of an fp32 index (default; FX_F32_SPLIT=0 scans the fp32
-    // rows with fp32 MFMA instead): rows [0, split_rows) are current.  L2
-    // indexes centre it (FX_CENTER=0: off): image rows fl(y - mu), their
-    // |.|^2 in cnorms (the scan's srcC), max in max_sq_bits[1]; mu = mean of a
-    // row sample, recomputed (and the image rebuilt) whenever ntotal has
-    // doubled since (mu_rows), so the centre follows the data at O(1)
-    // amortised cost per added row
-    DevBuf split, cnorms, centre, mu_part, qxn2;
-    int64_t split_rows = 0, mu_rows = 0;
+    DevBuf qin, qf32, qop, qeps, qrho, cand_d, cand_i, cand2_d, cand2_i, dws, iws, flag, fbc_d, fbc_i, stage, gtau,
+        trace, dbgbuf, stamps, pub;
+    // scan image (ImageKind; rows [0, img_rows) current).  L2 images are
+    // centred (Options.centre): mu = mean of a row sample, recomputed (and the
+    // image rebuilt) whenever ntotal has doubled since (mu_rows), so the
+    // centre follows the data at O(1) amortised cost per added row.
+    //   F32S: split = [hi | lo] bf16 planes of fl(y - mu), cnorms = |y - mu|^2
+    //   C16:  cnorms = |y - mu|^2 of the stored bf16 / fp16 rows (no copy of
+    //         the codes; a 16-bit centre whose norm is small next to the rows'
+    //         is set to 0 on the device: k_mu_finish)
+    DevBuf split, cnorms, centre, mu_part, qshift;
+    int64_t img_rows = 0, mu_rows = 0;
+    int img_kind = IMG_NONE;
     bool centred = false;
-    // FX_SEARCH_GRAPH=1: the search of a small host batch (the reference's
-    // one-query call form) replayed as one hipGraph per shape, over pinned
-    // host staging; `gkey` = the shape and every buffer the graph captured
+    // search_graph: the search of a small host batch (the reference's one-query
+    // call form) replayed as one hipGraph per shape, over pinned host staging;
+    // `gkey` = the shape and every buffer the graph captured
     hipGraphExec_t gexec = nullptr;
     std::vector<uint64_t> gkey;
     bool gfailed = false;
@@ -167,13 +231,7 @@ hipError_t grow(FxIndex* h, int64_t need_rows) {
     return hipSuccess;
 }
 
-// choose corpus splits per query tile: enough workgroups to fill 256 CUs
-// several times over (1 workgroup per CU resident: 129 KiB LDS)
-// k > KP: no cross-split pruning (ScanParams.share = 0) and at least k/4
-// splits, so that a split's KP-list rarely holds fewer than all of its top-k
-// rows and the certification bound (the smallest full split's KP-th key)
-// lies far beyond the k-th distance
-// split count whose live workgroups (one per CU: the scans' LDS) fill whole
+// split count whose live workgroups (one per CU: the scan's LDS) fill whole
 // rounds of 256 CUs best, with >= ~4 rounds and >= min_tiles tiles per split
 int fill_splits(int live_tiles, int eff_tiles, int n_ctiles, int min_tiles) {
     const int max_splits = std::max(1, n_ctiles / min_tiles);
@@ -190,48 +248,25 @@ int fill_splits(int live_tiles, int eff_tiles, int n_ctiles, int min_tiles) {
     return best;
 }
 
-// choose the scan kernel and its corpus splits per query tile
+// the scan's grid: corpus splits per query tile and block placement.
 // k > KP: no cross-split pruning (ScanParams.share = 0) and at least k/4
 // splits, so that a split's KP-list rarely holds fewer than all of its top-k
 // rows and the certification bound (the smallest full split's KP-th key)
 // lies far beyond the k-th distance
-void plan_scan(const FxIndex* h, int64_t nq, int k, int scan_dt, ScanParams& p) {
+void plan_scan(const FxIndex* h, int64_t nq, int k, ScanParams& p) {
     p.n_qtiles = (int)((nq + TILE_Q - 1) / TILE_Q);
     p.n_ctiles = (int)((h->ntotal + TILE_R - 1) / TILE_R);
-    p.q32_tiles = 0;
-    p.n_wtiles = 0;
     p.place = 0;
     p.sx = 0;
     p.pub = nullptr;
     p.prune_rank = KP;
     p.share = k <= KP ? 1 : 0;
-    const int rb64 = h->row_bytes / 64;
-    const char* q32_env = getenv("FX_SCAN_Q32");
-    if (q32_env && atoi(q32_env) == 1 && nq <= 32 && k <= KP && h->row_bytes % 64 == 0 &&
-        (rb64 == 8 || rb64 == 12 || rb64 == 16 || rb64 == 24)) {
-        // small batch (k_scan_q32): one 32-query tile; one round of one
-        // workgroup per CU, each split >= 4 tiles; every corpus byte read once
-        p.q32_tiles = (int)((nq + 31) / 32);
-        p.qt_per_xcd = 0;
-        p.splits = std::max(1, std::min(p.n_ctiles / 4, 256 / p.q32_tiles));
-        p.grid = p.q32_tiles * p.splits;
-        return;
-    }
-    // large batches: the wide-tile scan (192 queries per workgroup; FX_SCAN_W
-    // = 0 / 1 forces it off / on where it has a kernel for the row width)
-    const char* w_env = getenv("FX_SCAN_W");
-    const bool want_w = w_env ? atoi(w_env) == 1 : false;
-    const bool wide = want_w && scan_w_supported(scan_dt, h->row_bytes);
-    if (wide) p.n_wtiles = (int)((nq + scan_w_queries() - 1) / scan_w_queries());
-    const int ntl = wide ? p.n_wtiles : p.n_qtiles;              // query tiles of the chosen scan
-    const int nct = wide ? (int)((h->ntotal + 63) / 64) : p.n_ctiles;  // its corpus tiles
-    const int min_tiles = wide ? 8 : 4;
-    // placement (map_tile): FX_SCAN_PLACE = 0 / 1 forces query-tile groups /
-    // the corpus-partitioned form
-    // default: corpus-partitioned for k_scan_v4 (fewer corpus fetches past L2:
-    // 257 vs 742 GB per config (d) launch, and ~2 % faster)
-    const char* pl_env = getenv("FX_SCAN_PLACE");
-    const int place = pl_env ? atoi(pl_env) : (wide ? 0 : 1);
+    const int ntl = p.n_qtiles, nct = p.n_ctiles;
+    constexpr int min_tiles = 4;
+    // placement (map_tile): corpus-partitioned by default (config (d): 257 vs
+    // 742 GB fetched past L2 per launch, ~2 % faster); scan_place = 0 forces
+    // the query-tile groups of round 1
+    const int place = h->opt.place >= 0 ? h->opt.place : 1;
     if (place == 1 && ntl >= 8 && nct >= 8 * min_tiles) {
         // XCD x owns 1/8 of the corpus for every query tile; sx splits per
         // XCD so that its ntl * sx blocks fill whole rounds of its 32 CUs
@@ -246,8 +281,7 @@ void plan_scan(const FxIndex* h, int64_t nq, int k, int scan_dt, ScanParams& p) 
             if (eff > best_eff + 1e-9) { best_eff = eff; best = sx; }
             if (eff > 0.985 && live >= 128) break;
         }
-        // FX_SCAN_SX: splits per XCD, for placement A/B runs only
-        if (const char* sx_env = getenv("FX_SCAN_SX"); sx_env && *sx_env) best = std::max(1, std::min(max_sx, atoi(sx_env)));
+        if (h->opt.sx > 0) best = std::max(1, std::min(max_sx, h->opt.sx));  // placement A/B runs only
         if (k > KP) best = std::max(best, std::min(max_sx, ((k + 3) / 4 + 7) / 8));
         p.sx = best;
         p.splits = 8 * best;
@@ -265,10 +299,9 @@ void plan_scan(const FxIndex* h, int64_t nq, int k, int scan_dt, ScanParams& p) 
 int big_k1(int k) { return k > KP ? std::max(2 * k, 64) : 0; }
 
 // small batches over many splits: merge the candidate lists 16 splits at a
-// time before the refine (k_reduce_cand; FX_REDUCE_CAND=0 turns it off)
-bool use_reduce(int k, int64_t nq, int splits) {
-    const char* e = getenv("FX_REDUCE_CAND");
-    return k <= KP && nq <= 256 && splits >= 64 && !(e && atoi(e) == 0);
+// time before the refine (k_reduce_cand)
+bool use_reduce(const FxIndex* h, int k, int64_t nq, int splits) {
+    return k <= KP && nq <= 256 && splits >= 64 && h->opt.reduce_cand != 0;
 }
 
 hipError_t ensure_pinned_count(FxIndex* h) {
@@ -278,53 +311,234 @@ hipError_t ensure_pinned_count(FxIndex* h) {
     return e;
 }
 
-// fp32 index (unless FX_F32_SPLIT=0): bring its F32S scan image up to date
-// (rows appended since the last search); *split says whether the scan uses it
-hipError_t update_scan_image(FxIndex* h, bool* split) {
+// which scan image the index's current options call for
+int image_kind(const FxIndex* h) {
     const int rb64 = h->row_bytes / 64;
-    const char* split_env = getenv("FX_F32_SPLIT");
-    *split = !(split_env && atoi(split_env) == 0) && h->dtype == F32 && h->row_bytes % 64 == 0 &&
-             (rb64 == 8 || rb64 == 12 || rb64 == 16 || rb64 == 24);
-    if (!*split) return hipSuccess;
+    if (h->dtype == F32)
+        return h->opt.f32_split != 0 && h->row_bytes % 64 == 0 && (rb64 == 8 || rb64 == 12 || rb64 == 16 || rb64 == 24)
+                   ? IMG_F32S
+                   : IMG_NONE;
+    return h->metric == L2 && h->opt.centre != 0 ? IMG_C16 : IMG_NONE;
+}
+
+// bring the scan image up to date (rows appended since the last search)
+hipError_t update_scan_image(FxIndex* h) {
+    const int kind = image_kind(h);
     hipStream_t s = h->stream();
+    hipError_t e = hipSuccess;
+    if (kind == IMG_NONE) {
+        h->img_kind = IMG_NONE;
+        return hipSuccess;
+    }
     const void* old = h->split.p;
     const void* old_n = h->cnorms.p;
-    hipError_t e = h->split.ensure((size_t)h->cap_rows * h->row_bytes);
-    if (e == hipSuccess) e = h->cnorms.ensure((size_t)h->cap_rows * 4);
-    if (e != hipSuccess) return e;
-    bool rebuild = h->split.p != old || h->cnorms.p != old_n || h->split_rows > h->ntotal;
-    const char* ce = getenv("FX_CENTER");
-    const bool centre = h->metric == L2 && !(ce && atoi(ce) == 0);
+    if (kind == IMG_F32S && (e = h->split.ensure((size_t)h->cap_rows * h->row_bytes)) != hipSuccess) return e;
+    if ((e = h->cnorms.ensure((size_t)h->cap_rows * 4)) != hipSuccess) return e;
+    bool rebuild = h->split.p != old || h->cnorms.p != old_n || h->img_rows > h->ntotal || kind != h->img_kind;
+    const bool centre = h->metric == L2 && h->opt.centre != 0;
     if (centre != h->centred) rebuild = true;
-    if (centre && (h->mu_rows == 0 || h->ntotal >= 2 * h->mu_rows)) {
+    if (centre && (h->mu_rows == 0 || h->ntotal >= 2 * h->mu_rows || kind != h->img_kind)) {
         // (re)centre on the current rows
         if ((e = h->centre.ensure((size_t)h->kdim * 4)) != hipSuccess) return e;
-        if ((e = h->mu_part.ensure((size_t)MU_GROUPS * h->kdim * 8)) != hipSuccess) return e;
-        if ((e = launch_mu((const float*)h->codes, h->kdim, h->d, h->ntotal, (double*)h->mu_part.p, (float*)h->centre.p,
-                           s)) != hipSuccess)
+        if ((e = h->mu_part.ensure((size_t)2 * MU_GROUPS * h->kdim * 8)) != hipSuccess) return e;
+        // 16-bit rows: a centre whose norm is below 0.1 of the rows' mean
+        // square norm (no common direction) is dropped (mu = 0), which keeps
+        // 16-bit-exact queries exact in the scan operand
+        if ((e = launch_mu(h->codes, h->dtype, h->row_bytes, h->d, h->ntotal, (double*)h->mu_part.p,
+                           (float*)h->centre.p, kind == IMG_C16 ? 0.1f : 0.0f, s)) != hipSuccess)
             return e;
         h->mu_rows = h->ntotal;
         rebuild = true;
     }
     h->centred = centre;
+    h->img_kind = kind;
     if (rebuild) {  // zero image (finite padding rows), +inf padding norms
-        if ((e = hipMemsetAsync(h->split.p, 0, h->split.bytes, s)) != hipSuccess) return e;
+        if (kind == IMG_F32S && (e = hipMemsetAsync(h->split.p, 0, h->split.bytes, s)) != hipSuccess) return e;
         if ((e = hipMemsetD32Async((hipDeviceptr_t)h->cnorms.p, 0x7f800000u, h->cnorms.bytes / 4, s)) != hipSuccess)
             return e;
         if ((e = hipMemsetAsync(h->max_sq_bits + 1, 0, 4, s)) != hipSuccess) return e;
-        h->split_rows = 0;
+        h->img_rows = 0;
     }
-    e = launch_split_rows((const float*)h->codes, h->kdim, h->split_rows, h->ntotal,
-                          centre ? (const float*)h->centre.p : nullptr, h->split.p, (float*)h->cnorms.p,
-                          h->max_sq_bits + 1, s);
-    if (e == hipSuccess) h->split_rows = h->ntotal;
+    const float* mu = centre ? (const float*)h->centre.p : nullptr;
+    if (kind == IMG_F32S)
+        e = launch_split_rows((const float*)h->codes, h->kdim, h->img_rows, h->ntotal, mu, h->split.p,
+                              (float*)h->cnorms.p, h->max_sq_bits + 1, s);
+    else
+        e = launch_centre_norms(h->codes, h->dtype, h->row_bytes, h->img_rows, h->ntotal, mu, (float*)h->cnorms.p,
+                                h->max_sq_bits + 1, s);
+    if (e == hipSuccess) h->img_rows = h->ntotal;
     return e;
+}
+
+// The device-side plan of one search: scan, refine and fallback parameters
+// over the index's workspace.  Sizes the workspace (a no-op when it is large
+// enough already, as it is for a graph capture right after do_search).
+struct SearchPlan {
+    int64_t nq = 0, nq_pad = 0;
+    int k = 0, q_dtype = F32, scan_dt = F32;
+    ScanParams sp{};
+    RefineParams rp{};
+    PrepParams pp{};
+    bool reduce = false;
+    size_t ncand = 0;
+};
+
+hipError_t plan_search(FxIndex* h, int64_t nq, const void* qdev, int q_dtype, int k, float* Dd, int64_t* Id,
+                       SearchPlan& P) {
+    hipError_t e;
+    P.nq = nq;
+    P.k = k;
+    P.q_dtype = q_dtype;
+    P.nq_pad = round_up(nq, QPAD);
+    P.scan_dt = h->img_kind == IMG_F32S ? (int)F32S : h->dtype;
+    const bool img = h->img_kind != IMG_NONE;
+    if ((e = h->qf32.ensure((size_t)P.nq_pad * h->kdim * 4)) != hipSuccess) return e;
+    if ((e = h->qop.ensure((size_t)P.nq_pad * h->row_bytes)) != hipSuccess) return e;
+    if ((e = h->qeps.ensure((size_t)nq * 4)) != hipSuccess) return e;
+    if ((e = h->qrho.ensure((size_t)nq * 4)) != hipSuccess) return e;
+    if ((e = h->qshift.ensure((size_t)nq * 8)) != hipSuccess) return e;
+
+    PrepParams& pp = P.pp;
+    pp.q = qdev;
+    pp.q_dt = q_dtype;
+    pp.nq = nq;
+    pp.nq_pad = P.nq_pad;
+    pp.d = h->d;
+    pp.kdim = h->kdim;
+    pp.st_dt = P.scan_dt;
+    pp.metric = h->metric;
+    pp.qf32 = (float*)h->qf32.p;
+    pp.qop = h->qop.p;
+    pp.qeps = (float*)h->qeps.p;
+    pp.qrho = (float*)h->qrho.p;
+    pp.qshift = (double*)h->qshift.p;
+    pp.mbits = h->max_sq_bits;
+    pp.img_bits = img ? h->max_sq_bits + 1 : h->max_sq_bits;
+    pp.mu = img && h->centred ? (const float*)h->centre.p : nullptr;
+
+    ScanParams& sp = P.sp;
+    plan_scan(h, nq, k, sp);
+    sp.codes = h->img_kind == IMG_F32S ? (const char*)h->split.p : h->codes;
+    sp.norms = img ? (const float*)h->cnorms.p : h->norms;
+    sp.ntotal = h->ntotal;
+    sp.row_bytes = h->row_bytes;
+    sp.qop = (const char*)h->qop.p;
+    sp.nq = nq;
+    sp.dbg = h->opt.scan_dbg;
+    if ((e = h->gtau.ensure((size_t)P.nq_pad * 4)) != hipSuccess) return e;
+    sp.gtau = (unsigned*)h->gtau.p;
+    // k_scan_v4's published per-split lists (the union threshold, see
+    // compact_wave): slow-path tiles 25.7 -> 16.5 %, config (d) -3 %
+    if (sp.share && sp.splits > 1 && h->opt.pub != 0) {
+        const size_t npub = (size_t)sp.n_qtiles * TILE_Q * sp.splits * KP;
+        if ((e = h->pub.ensure(npub * 4)) != hipSuccess) return e;
+        sp.pub = (float*)h->pub.p;
+        // union bound taken at rank max(2k, 16) (<= KP): tighter pruning; the
+        // refine's certification bound is capped by the final threshold
+        sp.prune_rank = h->opt.prune_rank > 0 ? h->opt.prune_rank : std::max(2 * k, 16);
+        sp.prune_rank = std::max(k, std::min(KP, sp.prune_rank));
+    }
+    P.ncand = (size_t)sp.n_qtiles * sp.splits * TILE_Q * KP;
+    if ((e = h->cand_d.ensure(P.ncand * 4)) != hipSuccess) return e;
+    if ((e = h->cand_i.ensure(P.ncand * 4)) != hipSuccess) return e;
+    sp.cand_d = (float*)h->cand_d.p;
+    sp.cand_i = (int*)h->cand_i.p;
+    sp.trace = nullptr;
+    sp.dbgbuf = nullptr;
+    sp.stamps = nullptr;
+
+    if ((e = h->flag.ensure((size_t)(nq + 1) * 4)) != hipSuccess) return e;
+    RefineParams& rp = P.rp;
+    rp.cand_d = sp.cand_d;
+    rp.cand_i = sp.cand_i;
+    rp.splits = sp.splits;
+    rp.nq = nq;
+    rp.k = k;
+    rp.codes = h->codes;
+    rp.row_bytes = h->row_bytes;
+    rp.kdim = h->kdim;
+    rp.qf32 = pp.qf32;
+    rp.qeps = pp.qeps;
+    rp.qrho = pp.qrho;
+    rp.qshift = pp.qshift;
+    rp.id_offset = h->id_offset;
+    rp.D = Dd;
+    rp.I = Id;
+    rp.n_flag = (int*)h->flag.p;
+    rp.flag_list = rp.n_flag + 1;
+    // small batches: one wave per query walks splits * KP candidates (256 splits
+    // at nq = 1); issue 4 chunks of loads at a time (nq = 1: 0.84 -> ~0.3 ms)
+    rp.prefetch = nq <= 256 ? 4 : 1;
+    rp.k1 = big_k1(k);
+    rp.force_fb = h->opt.force_fallback;
+    rp.gtau = sp.share ? sp.gtau : nullptr;
+    P.reduce = use_reduce(h, k, nq, sp.splits);
+    if (P.reduce) {
+        const size_t nred = (size_t)sp.n_qtiles * ((sp.splits + 15) / 16) * TILE_Q * KP;
+        if ((e = h->cand2_d.ensure(nred * 4)) != hipSuccess) return e;
+        if ((e = h->cand2_i.ensure(nred * 4)) != hipSuccess) return e;
+    }
+    const size_t nfb = (size_t)std::max<int64_t>(4096, nq) * k;
+    if ((e = h->fbc_d.ensure(nfb * 4)) != hipSuccess) return e;
+    if ((e = h->fbc_i.ensure(nfb * 4)) != hipSuccess) return e;
+    return hipSuccess;
+}
+
+// Enqueue the planned search on s: query preparation, scan, candidate
+// reduction, refine + certification, device-gated exact fallback.  No host
+// synchronisation: the same sequence is what a search graph captures.
+hipError_t enqueue_search(FxIndex* h, SearchPlan& P, hipStream_t s, bool timed, hipEvent_t* ev) {
+    hipError_t e;
+    if ((e = launch_prep_queries(P.pp, s)) != hipSuccess) return e;
+    if ((e = hipMemsetD32Async((hipDeviceptr_t)P.sp.gtau, 0xff800000u, (size_t)P.nq_pad, s)) != hipSuccess)
+        return e;  // ord(+inf)
+    if (P.sp.pub) {
+        const size_t npub = (size_t)P.sp.n_qtiles * TILE_Q * P.sp.splits * KP;
+        if ((e = hipMemsetD32Async((hipDeviceptr_t)P.sp.pub, 0x7f800000u, npub, s)) != hipSuccess) return e;  // +inf
+    }
+    if (timed && (e = hipEventRecord(ev[0], s)) != hipSuccess) return e;
+    if ((e = launch_scan(P.scan_dt, h->metric, P.sp, s)) != hipSuccess) return e;
+    if (timed && (e = hipEventRecord(ev[1], s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(P.rp.n_flag, 0, 4, s)) != hipSuccess) return e;
+    RefineParams rp = P.rp;
+    if (P.reduce) {
+        int ng = 0;
+        if ((e = launch_reduce_cand(P.sp.cand_d, P.sp.cand_i, P.sp.splits, P.nq, P.sp.n_qtiles, (float*)h->cand2_d.p,
+                                    (int*)h->cand2_i.p, &ng, s)) != hipSuccess)
+            return e;
+        rp.cand_d = (const float*)h->cand2_d.p;
+        rp.cand_i = (const int*)h->cand2_i.p;
+        rp.splits = ng;
+    }
+    if ((e = launch_refine(h->dtype, h->metric, rp, s)) != hipSuccess) return e;
+    if (timed && (e = hipEventRecord(ev[2], s)) != hipSuccess) return e;
+    // Certification result: uncertified queries (rare: only when the
+    // candidate margin is inside the scan's rounding bound) are re-ranked by
+    // the exact scan.  Decided on the device: the fallback kernels are always
+    // enqueued and exit at once when the refine flagged nothing, so no host
+    // round trip sits inside the search.
+    if (P.sp.dbg == 0)
+        e = launch_exact_fallback(h->dtype, h->metric, h->codes, h->row_bytes, h->kdim, h->ntotal, P.rp.qf32,
+                                  P.rp.n_flag, P.k, h->id_offset, (float*)h->fbc_d.p, (int*)h->fbc_i.p, P.rp.D,
+                                  P.rp.I, s);
+    return e;
+}
+
+template <typename T>
+hipError_t dump_device(const std::string& path, const void* dev, size_t n) {
+    std::vector<T> v(n);
+    hipError_t e = hipMemcpy(v.data(), dev, n * sizeof(T), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return e;
+    if (FILE* f = fopen(path.c_str(), "ab")) {
+        fwrite(v.data(), sizeof(T), n, f);
+        fclose(f);
+    }
+    return hipSuccess;
 }
 
 int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int k, float* D, int64_t* I,
               int out_mem) {
     hipStream_t s = h->stream();
-    const int64_t nq_pad = round_up(nq, QPAD);
     const int qes = dtype_size(q_dtype);
     // queries -> device
     const void* qdev = q;
@@ -333,88 +547,6 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
         HIP_TRY(hipMemcpyAsync(h->qin.p, q, (size_t)nq * h->d * qes, hipMemcpyHostToDevice, s));
         qdev = h->qin.p;
     }
-    HIP_TRY(h->qf32.ensure((size_t)nq_pad * h->kdim * 4));
-    HIP_TRY(h->qop.ensure((size_t)nq_pad * h->row_bytes));
-    void* qop = h->qop.p;
-    HIP_TRY(h->qeps.ensure((size_t)nq * 4));
-    // fp32 index: scan it through its split-bf16 image (F32S:
-    // 3 bf16 products per term on the bf16 MFMA pipe instead of fp32 MFMA);
-    // the refine and the certification still use the fp32 rows
-    bool split = false;
-    HIP_TRY(update_scan_image(h, &split));
-    const int scan_dt = split ? (int)F32S : h->dtype;
-    HIP_TRY(h->qxn2.ensure((size_t)nq * 8));
-    HIP_TRY(launch_prep_queries(qdev, q_dtype, nq, nq_pad, h->d, h->kdim, scan_dt, h->metric, (float*)h->qf32.p,
-                                qop, (float*)h->qeps.p, h->max_sq_bits + (split ? 1 : 0),
-                                split && h->centred ? (const float*)h->centre.p : nullptr, (double*)h->qxn2.p, s));
-
-    ScanParams sp;
-    plan_scan(h, nq, k, scan_dt, sp);
-    sp.codes = split ? (const char*)h->split.p : h->codes;
-    sp.norms = split ? (const float*)h->cnorms.p : h->norms;
-    sp.ntotal = h->ntotal;
-    sp.row_bytes = h->row_bytes;
-    sp.qop = (const char*)qop;
-    sp.nq = nq;
-    sp.dbg = getenv("FX_SCAN_DBG") ? atoi(getenv("FX_SCAN_DBG")) : 0;
-    HIP_TRY(h->gtau.ensure((size_t)nq_pad * 4));
-    sp.gtau = (unsigned*)h->gtau.p;
-    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)sp.gtau, 0xff800000u, (size_t)nq_pad, s));  // ord(+inf)
-    // k_scan_v4's published per-split lists (the union threshold, see
-    // compact_wave): slow-path tiles 25.7 -> 16.5 %, config (d) -3 %;
-    // FX_SCAN_PUB=0 turns them off
-    const char* pub_env = getenv("FX_SCAN_PUB");
-    if (sp.share && sp.q32_tiles == 0 && sp.n_wtiles == 0 && sp.splits > 1 && !(pub_env && atoi(pub_env) == 0)) {
-        const size_t npub = (size_t)sp.n_qtiles * TILE_Q * sp.splits * KP;
-        HIP_TRY(h->pub.ensure(npub * 4));
-        HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)h->pub.p, 0x7f800000u, npub, s));  // +inf: no entry
-        sp.pub = (float*)h->pub.p;
-        // union bound taken at rank max(2k, 16) (<= KP): tighter pruning; the
-        // refine's certification bound is capped by the final threshold
-        const char* rk_env = getenv("FX_PRUNE_RANK");
-        sp.prune_rank = rk_env ? atoi(rk_env) : std::max(2 * k, 16);
-        sp.prune_rank = std::max(k, std::min(KP, sp.prune_rank));
-    }
-    const int cand_splits = sp.splits;  // one candidate list per (query, split)
-    const size_t ncand = (size_t)sp.n_qtiles * cand_splits * TILE_Q * KP;
-    HIP_TRY(h->cand_d.ensure(ncand * 4));
-    HIP_TRY(h->cand_i.ensure(ncand * 4));
-    sp.cand_d = (float*)h->cand_d.p;
-    sp.cand_i = (int*)h->cand_i.p;
-    // diagnostics: per-block placement/timing of the scan -> binary file
-    const char* trace_path = getenv("FX_SCAN_TRACE");
-    const size_t grid = (size_t)sp.grid;
-    sp.trace = nullptr;
-    sp.dbgbuf = nullptr;
-    sp.stamps = nullptr;
-    const char* stamp_path = getenv("FX_SCAN_STAMPS");
-    if (stamp_path) {
-        HIP_TRY(h->stamps.ensure(grid * 4 * 128));
-        HIP_TRY(hipMemsetAsync(h->stamps.p, 0, grid * 4 * 128, s));
-        sp.stamps = (unsigned long long*)h->stamps.p;
-    }
-    const size_t nkeys = (size_t)sp.n_qtiles * TILE_Q * sp.n_ctiles * TILE_R;
-    if ((sp.dbg & 32) && nkeys <= (size_t)1 << 26) {
-        HIP_TRY(h->dbgbuf.ensure(nkeys * 4));
-        HIP_TRY(hipMemsetAsync(h->dbgbuf.p, 0xff, nkeys * 4, s));
-        sp.dbgbuf = (unsigned*)h->dbgbuf.p;
-    }
-    if (trace_path) {
-        HIP_TRY(h->trace.ensure(grid * 32));
-        HIP_TRY(hipMemsetAsync(h->trace.p, 0, grid * 32, s));
-        sp.trace = (unsigned long long*)h->trace.p;
-    }
-
-    hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
-    if (h->profile) {
-        HIP_TRY(hipEventCreate(&e0));
-        HIP_TRY(hipEventCreate(&e1));
-        HIP_TRY(hipEventCreate(&e2));
-        HIP_TRY(hipEventRecord(e0, s));
-    }
-    HIP_TRY(launch_scan(scan_dt, h->metric, sp, s));
-    if (h->profile) HIP_TRY(hipEventRecord(e1, s));
-
     float* Dd = D;
     int64_t* Id = I;
     if (out_mem == FX_MEM_HOST) {
@@ -423,101 +555,59 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
         Dd = (float*)h->dws.p;
         Id = (int64_t*)h->iws.p;
     }
-    HIP_TRY(h->flag.ensure((size_t)(nq + 1) * 4));
-    int* n_flag = (int*)h->flag.p;
-    HIP_TRY(hipMemsetAsync(n_flag, 0, 4, s));
-
-    RefineParams rp;
-    rp.cand_d = sp.cand_d;
-    rp.cand_i = sp.cand_i;
-    rp.splits = cand_splits;
-    rp.nq = nq;
-    rp.k = k;
-    rp.codes = h->codes;
-    rp.row_bytes = h->row_bytes;
-    rp.kdim = h->kdim;
-    rp.qf32 = (const float*)h->qf32.p;
-    rp.qeps = (const float*)h->qeps.p;
-    rp.qxn2 = (const double*)h->qxn2.p;
-    rp.id_offset = h->id_offset;
-    rp.D = Dd;
-    rp.I = Id;
-    rp.n_flag = n_flag;
-    rp.flag_list = n_flag + 1;
-    // small batches: one wave per query walks splits * KP candidates (256 splits
-    // at nq = 1); issue 4 chunks of loads at a time (nq = 1: 0.84 -> ~0.3 ms)
-    rp.prefetch = (sp.q32_tiles > 0 || nq <= 256) ? 4 : 1;
-    rp.k1 = big_k1(k);
-    rp.force_fb = getenv("FX_FORCE_FALLBACK") ? atoi(getenv("FX_FORCE_FALLBACK")) : 0;
-    rp.gtau = sp.share ? sp.gtau : nullptr;
-    if (use_reduce(k, nq, cand_splits)) {
-        const size_t nred = (size_t)sp.n_qtiles * ((cand_splits + 15) / 16) * TILE_Q * KP;
-        HIP_TRY(h->cand2_d.ensure(nred * 4));
-        HIP_TRY(h->cand2_i.ensure(nred * 4));
-        int ng = 0;
-        HIP_TRY(launch_reduce_cand(sp.cand_d, sp.cand_i, cand_splits, nq, sp.n_qtiles, (float*)h->cand2_d.p,
-                                   (int*)h->cand2_i.p, &ng, s));
-        rp.cand_d = (const float*)h->cand2_d.p;
-        rp.cand_i = (const int*)h->cand2_i.p;
-        rp.splits = ng;
+    HIP_TRY(update_scan_image(h));
+    SearchPlan P;
+    HIP_TRY(plan_search(h, nq, qdev, q_dtype, k, Dd, Id, P));
+    // diagnostics (Options): per-block placement/timing, phase stamps, the
+    // scan's key matrix, raw candidate lists -> binary files
+    const size_t grid = (size_t)P.sp.grid;
+    if (!h->opt.stamps.empty()) {
+        HIP_TRY(h->stamps.ensure(grid * 4 * 128));
+        HIP_TRY(hipMemsetAsync(h->stamps.p, 0, grid * 4 * 128, s));
+        P.sp.stamps = (unsigned long long*)h->stamps.p;
     }
-    HIP_TRY(launch_refine(h->dtype, h->metric, rp, s));
+    const size_t nkeys = (size_t)P.sp.n_qtiles * TILE_Q * P.sp.n_ctiles * TILE_R;
+    if ((P.sp.dbg & 32) && nkeys <= (size_t)1 << 26) {
+        HIP_TRY(h->dbgbuf.ensure(nkeys * 4));
+        HIP_TRY(hipMemsetAsync(h->dbgbuf.p, 0xff, nkeys * 4, s));
+        P.sp.dbgbuf = (unsigned*)h->dbgbuf.p;
+    }
+    if (!h->opt.trace.empty()) {
+        HIP_TRY(h->trace.ensure(grid * 32));
+        HIP_TRY(hipMemsetAsync(h->trace.p, 0, grid * 32, s));
+        P.sp.trace = (unsigned long long*)h->trace.p;
+    }
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    if (h->profile)
+        for (auto& x : ev) HIP_TRY(hipEventCreate(&x));
+    HIP_TRY(enqueue_search(h, P, s, h->profile, ev));
     if (h->profile) {
-        HIP_TRY(hipEventRecord(e2, s));
-        h->ev_scan.emplace_back(e0, e1);
-        h->ev_merge.emplace_back(e1, e2);
-    }
-
-    // Certification result: uncertified queries (rare: only when the
-    // candidate margin is inside the scan's worst-case rounding bound) are
-    // re-ranked by the exact fp64 scan.  Decided on the device: both
-    // fallback kernels are always enqueued and exit at once when the refine
-    // flagged nothing, so no host round trip sits inside the search.
-    if (sp.dbg == 0) {
-        const size_t nfb = (size_t)std::max<int64_t>(4096, nq) * k;
-        HIP_TRY(h->fbc_d.ensure(nfb * 4));
-        HIP_TRY(h->fbc_i.ensure(nfb * 4));
-        HIP_TRY(launch_exact_fallback(h->dtype, h->metric, h->codes, h->row_bytes, h->kdim, h->ntotal,
-                                      (const float*)h->qf32.p, n_flag, k, h->id_offset, (float*)h->fbc_d.p,
-                                      (int*)h->fbc_i.p, Dd, Id, s));
+        h->ev_scan.emplace_back(ev[0], ev[1]);
+        h->ev_merge.emplace_back(ev[1], ev[2]);
     }
     HIP_TRY(ensure_pinned_count(h));
-    HIP_TRY(hipMemcpyAsync(h->pin_nf, n_flag, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(h->pin_nf, P.rp.n_flag, 4, hipMemcpyDeviceToHost, s));
     h->fb_pending = true;
-    if (const char* cpath = getenv("FX_SCAN_CAND")) {  // diagnostics: raw scan candidate lists
-        std::vector<float> cd(ncand);
-        std::vector<int> ci(ncand);
-        HIP_TRY(hipMemcpy(cd.data(), sp.cand_d, ncand * 4, hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemcpy(ci.data(), sp.cand_i, ncand * 4, hipMemcpyDeviceToHost));
-        if (FILE* f = fopen(cpath, "wb")) {
-            fwrite(cd.data(), 4, ncand, f);
-            fwrite(ci.data(), 4, ncand, f);
-            fclose(f);
-        }
+    if (!h->opt.cand.empty()) {
+        HIP_TRY(hipStreamSynchronize(s));
+        HIP_TRY(dump_device<float>(h->opt.cand, P.sp.cand_d, P.ncand));
+        HIP_TRY(dump_device<int>(h->opt.cand, P.sp.cand_i, P.ncand));
     }
-    if (sp.dbgbuf) {  // diagnostics: the scan's key matrix [n_qtiles*128][n_ctiles*128] -> file
-        std::vector<float> kv(nkeys);
-        HIP_TRY(hipMemcpy(kv.data(), sp.dbgbuf, nkeys * 4, hipMemcpyDeviceToHost));
-        if (FILE* f = fopen(getenv("FX_SCAN_KEYS") ? getenv("FX_SCAN_KEYS") : "/tmp/fx_keys.bin", "wb")) {
-            fwrite(kv.data(), 4, kv.size(), f);
-            fclose(f);
-        }
+    if (P.sp.dbgbuf) {  // the scan's key matrix [n_qtiles*128][n_ctiles*128]
+        HIP_TRY(hipStreamSynchronize(s));
+        const std::string path = h->opt.keys.empty() ? std::string("/tmp/fx_keys.bin") : h->opt.keys;
+        if (FILE* f = fopen(path.c_str(), "wb")) fclose(f);  // truncate: one dump per search
+        HIP_TRY(dump_device<float>(path, P.sp.dbgbuf, nkeys));
     }
-    if (sp.stamps) {
-        std::vector<unsigned long long> st(grid * 4 * 16);
-        HIP_TRY(hipMemcpy(st.data(), sp.stamps, grid * 4 * 128, hipMemcpyDeviceToHost));
-        if (FILE* f = fopen(stamp_path, "wb")) {
-            fwrite(st.data(), 8, st.size(), f);
-            fclose(f);
-        }
+    if (P.sp.stamps) {
+        HIP_TRY(hipStreamSynchronize(s));
+        if (FILE* f = fopen(h->opt.stamps.c_str(), "wb")) fclose(f);
+        HIP_TRY(dump_device<unsigned long long>(h->opt.stamps, P.sp.stamps, grid * 4 * 16));
     }
-    if (sp.trace) {
-        std::vector<unsigned long long> tr(grid * 4);
-        HIP_TRY(hipMemcpy(tr.data(), sp.trace, grid * 32, hipMemcpyDeviceToHost));
-        if (FILE* f = fopen(trace_path, "wb")) {
-            fwrite(tr.data(), 8, tr.size(), f);
-            fclose(f);
-        }
+    if (P.sp.trace) {
+        HIP_TRY(hipStreamSynchronize(s));
+        if (FILE* f = fopen(h->opt.trace.c_str(), "wb")) fclose(f);
+        HIP_TRY(dump_device<unsigned long long>(h->opt.trace, P.sp.trace, grid * 4));
     }
     if (out_mem == FX_MEM_HOST) {
         HIP_TRY(hipMemcpyAsync(D, Dd, (size_t)nq * k * 4, hipMemcpyDeviceToHost, s));
@@ -529,23 +619,20 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
     return FX_OK;
 }
 
-// Shape + every device buffer a captured search touches: the graph is valid
-// while all of them are unchanged
-std::vector<uint64_t> graph_key(const FxIndex* h, int64_t nq, int q_dtype, int k, int scan_dt) {
-    ScanParams sp;
-    plan_scan(h, nq, k, scan_dt, sp);
-    const char* se = getenv("FX_F32_SPLIT");  // (part of the key: unset and "1" both mean on)
+// Shape + options + every device buffer a captured search touches: the graph
+// is valid while all of them are unchanged
+std::vector<uint64_t> graph_key(const FxIndex* h, int64_t nq, int q_dtype, int k) {
+    const Options& o = h->opt;
     return {(uint64_t)nq, (uint64_t)q_dtype, (uint64_t)k, (uint64_t)h->ntotal, (uint64_t)h->id_offset,
-            (uint64_t)(se ? atoi(se) : 1),
-            (uint64_t)(getenv("FX_FORCE_FALLBACK") ? atoi(getenv("FX_FORCE_FALLBACK")) : 0),
-            (uint64_t)sp.splits, (uint64_t)sp.q32_tiles, (uint64_t)sp.qt_per_xcd, (uint64_t)sp.n_wtiles,
-            (uint64_t)sp.place, (uint64_t)sp.sx, (uint64_t)sp.grid,
+            (uint64_t)h->img_kind, (uint64_t)h->centred, (uint64_t)h->img_rows,
+            (uint64_t)o.force_fallback, (uint64_t)o.place, (uint64_t)o.sx, (uint64_t)o.reduce_cand,
+            (uint64_t)o.pub, (uint64_t)o.prune_rank,
             (uint64_t)(uintptr_t)h->codes, (uint64_t)(uintptr_t)h->norms, (uint64_t)(uintptr_t)h->split.p,
-            (uint64_t)(uintptr_t)h->cnorms.p, (uint64_t)(uintptr_t)h->centre.p, (uint64_t)(uintptr_t)h->qxn2.p,
-            (uint64_t)h->centred,
+            (uint64_t)(uintptr_t)h->cnorms.p, (uint64_t)(uintptr_t)h->centre.p, (uint64_t)(uintptr_t)h->qshift.p,
             (uint64_t)(uintptr_t)h->qin.p, (uint64_t)(uintptr_t)h->qf32.p, (uint64_t)(uintptr_t)h->qop.p,
-            (uint64_t)(uintptr_t)h->qeps.p, (uint64_t)(uintptr_t)h->gtau.p, (uint64_t)(uintptr_t)h->cand_d.p,
-            (uint64_t)(uintptr_t)h->cand_i.p, (uint64_t)(uintptr_t)h->cand2_d.p, (uint64_t)(uintptr_t)h->cand2_i.p,
+            (uint64_t)(uintptr_t)h->qeps.p, (uint64_t)(uintptr_t)h->qrho.p, (uint64_t)(uintptr_t)h->gtau.p,
+            (uint64_t)(uintptr_t)h->pub.p, (uint64_t)(uintptr_t)h->cand_d.p, (uint64_t)(uintptr_t)h->cand_i.p,
+            (uint64_t)(uintptr_t)h->cand2_d.p, (uint64_t)(uintptr_t)h->cand2_i.p,
             (uint64_t)(uintptr_t)h->dws.p, (uint64_t)(uintptr_t)h->iws.p,
             (uint64_t)(uintptr_t)h->flag.p, (uint64_t)(uintptr_t)h->fbc_d.p, (uint64_t)(uintptr_t)h->fbc_i.p};
 }
@@ -558,8 +645,9 @@ void graph_release(FxIndex* h) {
 
 // Record the stream-ordered search of do_search (host queries, host results,
 // no diagnostics) into h->gexec.  Runs right after a do_search of the same
-// shape, so every workspace is sized and every kernel attribute set.
-hipError_t graph_build(FxIndex* h, int64_t nq, int q_dtype, int k, bool split) {
+// shape, so every workspace is sized and every kernel attribute set; the
+// enqueued sequence is do_search's own (enqueue_search).
+hipError_t graph_build(FxIndex* h, int64_t nq, int q_dtype, int k) {
     graph_release(h);
     hipStream_t s = h->stream();
     const size_t qb = (size_t)nq * h->d * dtype_size(q_dtype), nd = (size_t)nq * k;
@@ -582,76 +670,18 @@ hipError_t graph_build(FxIndex* h, int64_t nq, int q_dtype, int k, bool split) {
         h->ghd_n = nd;
     }
     if (!h->ghnf && (e = hipHostMalloc((void**)&h->ghnf, 4, hipHostMallocDefault)) != hipSuccess) return e;
-
-    const int scan_dt = split ? (int)F32S : h->dtype;
-    const int64_t nq_pad = round_up(nq, QPAD);
-    ScanParams sp;
-    plan_scan(h, nq, k, scan_dt, sp);
-    sp.codes = split ? (const char*)h->split.p : h->codes;
-    sp.norms = split ? (const float*)h->cnorms.p : h->norms;
-    sp.ntotal = h->ntotal;
-    sp.row_bytes = h->row_bytes;
-    sp.qop = (const char*)h->qop.p;
-    sp.nq = nq;
-    sp.dbg = 0;
-    sp.gtau = (unsigned*)h->gtau.p;
-    sp.cand_d = (float*)h->cand_d.p;
-    sp.cand_i = (int*)h->cand_i.p;
-    sp.trace = nullptr;
-    sp.dbgbuf = nullptr;
-    sp.stamps = nullptr;
-    int* n_flag = (int*)h->flag.p;
-    RefineParams rp;
-    rp.cand_d = sp.cand_d;
-    rp.cand_i = sp.cand_i;
-    rp.splits = sp.splits;
-    rp.nq = nq;
-    rp.k = k;
-    rp.codes = h->codes;
-    rp.row_bytes = h->row_bytes;
-    rp.kdim = h->kdim;
-    rp.qf32 = (const float*)h->qf32.p;
-    rp.qeps = (const float*)h->qeps.p;
-    rp.qxn2 = (const double*)h->qxn2.p;
-    rp.id_offset = h->id_offset;
-    rp.D = (float*)h->dws.p;
-    rp.I = (int64_t*)h->iws.p;
-    rp.n_flag = n_flag;
-    rp.flag_list = n_flag + 1;
-    // small batches: one wave per query walks splits * KP candidates (256 splits
-    // at nq = 1); issue 4 chunks of loads at a time (nq = 1: 0.84 -> ~0.3 ms)
-    rp.prefetch = (sp.q32_tiles > 0 || nq <= 256) ? 4 : 1;
-    rp.k1 = big_k1(k);
-    rp.force_fb = getenv("FX_FORCE_FALLBACK") ? atoi(getenv("FX_FORCE_FALLBACK")) : 0;
-    rp.gtau = sp.share ? sp.gtau : nullptr;
+    SearchPlan P;
+    if ((e = plan_search(h, nq, h->qin.p, q_dtype, k, (float*)h->dws.p, (int64_t*)h->iws.p, P)) != hipSuccess)
+        return e;
+    P.sp.dbg = 0;
 
     if ((e = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal)) != hipSuccess) return e;
     g_graph_capture = true;
     hipError_t ce = hipMemcpyAsync(h->qin.p, h->ghq, qb, hipMemcpyHostToDevice, s);
-    if (ce == hipSuccess)
-        ce = launch_prep_queries(h->qin.p, q_dtype, nq, nq_pad, h->d, h->kdim, scan_dt, h->metric, (float*)h->qf32.p,
-                                 h->qop.p, (float*)h->qeps.p, h->max_sq_bits + (split ? 1 : 0),
-                                 split && h->centred ? (const float*)h->centre.p : nullptr, (double*)h->qxn2.p, s);
-    if (ce == hipSuccess)
-        ce = hipMemsetD32Async((hipDeviceptr_t)sp.gtau, 0xff800000u, (size_t)nq_pad, s);
-    if (ce == hipSuccess) ce = launch_scan(scan_dt, h->metric, sp, s);
-    if (ce == hipSuccess) ce = hipMemsetAsync(n_flag, 0, 4, s);
-    if (ce == hipSuccess && use_reduce(k, nq, sp.splits)) {  // sized by the preceding do_search
-        int ng = 0;
-        ce = launch_reduce_cand(sp.cand_d, sp.cand_i, sp.splits, nq, sp.n_qtiles, (float*)h->cand2_d.p,
-                                (int*)h->cand2_i.p, &ng, s);
-        rp.cand_d = (const float*)h->cand2_d.p;
-        rp.cand_i = (const int*)h->cand2_i.p;
-        rp.splits = ng;
-    }
-    if (ce == hipSuccess) ce = launch_refine(h->dtype, h->metric, rp, s);
-    if (ce == hipSuccess)
-        ce = launch_exact_fallback(h->dtype, h->metric, h->codes, h->row_bytes, h->kdim, h->ntotal,
-                                   (const float*)h->qf32.p, n_flag, k, h->id_offset, (float*)h->fbc_d.p,
-                                   (int*)h->fbc_i.p, rp.D, rp.I, s);
-    if (ce == hipSuccess) ce = hipMemcpyAsync(h->ghD, rp.D, nd * 4, hipMemcpyDeviceToHost, s);
-    if (ce == hipSuccess) ce = hipMemcpyAsync(h->ghI, rp.I, nd * 8, hipMemcpyDeviceToHost, s);
-    if (ce == hipSuccess) ce = hipMemcpyAsync(h->ghnf, n_flag, 4, hipMemcpyDeviceToHost, s);
+    if (ce == hipSuccess) ce = enqueue_search(h, P, s, false, nullptr);
+    if (ce == hipSuccess) ce = hipMemcpyAsync(h->ghD, P.rp.D, nd * 4, hipMemcpyDeviceToHost, s);
+    if (ce == hipSuccess) ce = hipMemcpyAsync(h->ghI, P.rp.I, nd * 8, hipMemcpyDeviceToHost, s);
+    if (ce == hipSuccess) ce = hipMemcpyAsync(h->ghnf, P.rp.n_flag, 4, hipMemcpyDeviceToHost, s);
     g_graph_capture = false;
     hipGraph_t graph = nullptr;
     e = hipStreamEndCapture(s, &graph);  // always end the capture: the stream must leave capture mode
@@ -663,17 +693,16 @@ hipError_t graph_build(FxIndex* h, int64_t nq, int q_dtype, int k, bool split) {
         (void)hipGetLastError();
         return e;
     }
-    h->gkey = graph_key(h, nq, q_dtype, k, scan_dt);
+    h->gkey = graph_key(h, nq, q_dtype, k);
     return hipSuccess;
 }
 
-// Small host batches under FX_SEARCH_GRAPH=1: replay the captured search
-// (the exact fallback included: it is device-gated); on a shape / buffer
+// Small host batches under search_graph: replay the captured search (the
+// exact fallback included: it is device-gated); on a shape / buffer / option
 // change run do_search and re-capture.
 int graph_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int k, float* D, int64_t* I) {
-    bool split = false;
-    HIP_TRY(update_scan_image(h, &split));
-    if (h->gexec && graph_key(h, nq, q_dtype, k, split ? (int)F32S : h->dtype) == h->gkey) {
+    HIP_TRY(update_scan_image(h));
+    if (h->gexec && graph_key(h, nq, q_dtype, k) == h->gkey) {
         hipStream_t s = h->stream();
         memcpy(h->ghq, q, (size_t)nq * h->d * dtype_size(q_dtype));
         HIP_TRY(hipGraphLaunch(h->gexec, s));
@@ -686,11 +715,11 @@ int graph_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int k, floa
     }
     const int rc = do_search(h, nq, q, q_dtype, FX_MEM_HOST, k, D, I, FX_MEM_HOST);
     if (rc == FX_OK && !h->gfailed) {
-        const hipError_t e = graph_build(h, nq, q_dtype, k, split);
+        const hipError_t e = graph_build(h, nq, q_dtype, k);
         if (e != hipSuccess) {  // stay on do_search for this index
             h->gfailed = true;
-            if (getenv("FX_SEARCH_GRAPH_VERBOSE")) fprintf(stderr, "fx: search graph capture failed: %s\n", hipGetErrorString(e));
-        } else if (getenv("FX_SEARCH_GRAPH_VERBOSE")) {
+            if (h->opt.graph_verbose) fprintf(stderr, "fx: search graph capture failed: %s\n", hipGetErrorString(e));
+        } else if (h->opt.graph_verbose) {
             fprintf(stderr, "fx: search graph captured (nq=%lld k=%d)\n", (long long)nq, k);
         }
     }
@@ -734,10 +763,12 @@ int fx_index_create(int d, int storage_dtype, int metric, int device, FxIndex** 
     h->device = device;
     h->row_bytes = (int)round_up((int64_t)d * dtype_size(storage_dtype), ROW_ALIGN);
     h->kdim = h->row_bytes / dtype_size(storage_dtype);
+    h->opt.from_env();
     // A BLOCKING stream: work on the legacy null stream (torch's default
     // stream, cuda_stream == 0) is ordered before and after it, so a caller
     // that binds "stream 0" (fx_index_set_stream(h, NULL)) stays ordered.
     hipError_t e = hipStreamCreateWithFlags(&h->own_stream, hipStreamDefault);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->switch_ev, hipEventDisableTiming);
     if (e == hipSuccess) e = hipMalloc(&h->max_sq_bits, 16);
     if (e == hipSuccess) e = hipMemset(h->max_sq_bits, 0, 16);
     if (e != hipSuccess) {
@@ -759,7 +790,8 @@ void fx_index_free(FxIndex* h) {
         if (h->max_sq_bits) (void)hipFree(h->max_sq_bits);
         for (DevBuf* b : {&h->qin, &h->qf32, &h->qop, &h->qeps, &h->cand_d, &h->cand_i, &h->dws, &h->iws, &h->flag,
                           &h->fbc_d, &h->fbc_i, &h->stage, &h->gtau, &h->trace, &h->dbgbuf, &h->split, &h->cnorms,
-                          &h->centre, &h->mu_part, &h->qxn2, &h->stamps, &h->pub, &h->cand2_d, &h->cand2_i})
+                          &h->centre, &h->mu_part, &h->qshift, &h->qrho, &h->stamps, &h->pub, &h->cand2_d,
+                          &h->cand2_i})
             b->release();
         graph_release(h);
         if (h->ghq) (void)hipHostFree(h->ghq);
@@ -769,6 +801,7 @@ void fx_index_free(FxIndex* h) {
         if (h->pin_nf) (void)hipHostFree(h->pin_nf);
         for (auto& pr : h->ev_scan) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
         for (auto& pr : h->ev_merge) (void)hipEventDestroy(pr.second);
+        if (h->switch_ev) (void)hipEventDestroy(h->switch_ev);
         if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
     }
     delete h;
@@ -784,7 +817,25 @@ int fx_index_set_normalize(FxIndex* h, int on) {
 int fx_index_set_stream(FxIndex* h, void* stream) {
     if (!h) return set_err(FX_E_ARG, "null index");
     std::lock_guard<std::mutex> lk(h->mu);
+    const hipStream_t prev = h->stream();
     h->user_stream = (hipStream_t)stream;
+    const hipStream_t next = h->stream();
+    if (next != prev) {
+        // the index's work stays in call order across a stream switch: the new
+        // stream waits (on the device) for everything enqueued on the old one
+        DeviceGuard g(h->device);
+        HIP_TRY(hipEventRecord(h->switch_ev, prev));
+        HIP_TRY(hipStreamWaitEvent(next, h->switch_ev, 0));
+    }
+    return FX_OK;
+}
+
+int fx_index_set_option(FxIndex* h, const char* name, int64_t value) {
+    if (!h || !name) return set_err(FX_E_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(h->mu);
+    int* slot = h->opt.find(name);
+    if (!slot) return set_err(FX_E_ARG, "unknown option '%s'", name);
+    *slot = (int)value;
     return FX_OK;
 }
 
@@ -885,9 +936,9 @@ int fx_index_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_me
         h->fb_pending = false;
         return FX_OK;
     }
-    const char* ge = getenv("FX_SEARCH_GRAPH");
-    if (ge && atoi(ge) == 1 && q_mem == FX_MEM_HOST && out_mem == FX_MEM_HOST && nq <= 64 && !h->profile &&
-        !getenv("FX_SCAN_DBG") && !getenv("FX_SCAN_TRACE") && !getenv("FX_SCAN_CAND") && h->user_stream == nullptr)
+    const Options& o = h->opt;
+    if (o.search_graph == 1 && q_mem == FX_MEM_HOST && out_mem == FX_MEM_HOST && nq <= 64 && !h->profile &&
+        o.scan_dbg == 0 && o.trace.empty() && o.cand.empty() && o.stamps.empty() && h->user_stream == nullptr)
         return graph_search(h, nq, q, q_dtype, k, D, I);
     return do_search(h, nq, q, q_dtype, q_mem, k, D, I, out_mem);
 }
@@ -916,7 +967,7 @@ int fx_index_reset(FxIndex* h) {
         HIP_TRY(hipMemsetD32((hipDeviceptr_t)h->norms, 0x7f800000u, (size_t)h->cap_rows));
     }
     h->ntotal = 0;
-    h->split_rows = 0;
+    h->img_rows = 0;
     h->mu_rows = 0;
     return FX_OK;
 }

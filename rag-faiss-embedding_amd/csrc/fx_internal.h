@@ -56,12 +56,8 @@ struct ScanParams {
     unsigned long long* trace;  // diagnostics only (FX_SCAN_TRACE): per block
                                 // {xcc | hw_id << 8 | qtile << 32, split, t_start, t_end}
     unsigned* dbgbuf;           // diagnostics only (FX_SCAN_DBG & 32): operand self-check
-    int q32_tiles;              // > 0: small-batch scan k_scan_q32 (FX_SCAN_Q32=1) over this many
-                                // 32-query tiles (one workgroup per tile and split)
     int share;                  // 1: splits publish their KP-th key to gtau and prune with it
                                 // (k <= KP); 0: no cross-split pruning (k > KP, k_refine_big)
-    int n_wtiles;               // > 0: wide scan k_scan_w (fx_scan_w.hip) over this many tiles of
-                                // scan_w_queries() queries (qt_per_xcd then counts wide tiles)
     int place;                  // block placement (map_tile): 0 query-tile groups per XCD, 1
                                 // corpus-partitioned (XCD x owns splits [x sx, (x+1) sx))
     int sx;                     // place 1: corpus splits per XCD (splits = 8 sx)
@@ -73,9 +69,8 @@ struct ScanParams {
                                 // [grid][4 waves][16] per-wave cycle sums of the scan's phases
 };
 
-// queries are zero-padded to a multiple of QPAD (a multiple of every scan's
-// query tile: 128, and the wide scan's 192)
-constexpr int QPAD = 768;
+// queries are zero-padded to a multiple of QPAD (the scan's query tile)
+constexpr int QPAD = TILE_Q;
 
 struct RefineParams {
     const float* cand_d;   // scan output (approx keys)
@@ -87,8 +82,10 @@ struct RefineParams {
     int row_bytes;
     int kdim;
     const float* qf32;     // [nq_pad][kdim] fp32 queries, zero padded
-    const float* qeps;     // [nq] certification margin
-    const double* qxn2;    // [nq] |x - mu|^2 (mu: the scan image's centre, 0 if none)
+    const float* qeps;     // [nq] E: query-wide bound on |approx key + shift - exact|
+    const float* qrho;     // [nq] rho = |x - mu - x_op| (the scan operand's rounding): the bound adds
+                           // 2 rho sqrt(D) for a row at exact distance D (L2, 16-bit / fp32 rows)
+    const double* qshift;  // [nq] s_q: approx key + s_q estimates the exact distance
     int64_t id_offset;
     float* D;              // [nq][k]
     int64_t* I;
@@ -122,19 +119,28 @@ extern thread_local bool g_graph_capture;
 hipError_t launch_convert_rows(const void* x, int x_dt, int64_t n, int d, void* codes_row0, int st_dt,
                                int kdim, float* norms_row0, unsigned* max_sq_bits, int normalize,
                                hipStream_t s);
-// mu: centre of a centred F32S image (null: none); qxn2[nq] <- |x - mu|^2 (fp64)
-hipError_t launch_prep_queries(const void* q, int q_dt, int64_t nq, int64_t nq_pad, int d, int kdim,
-                               int st_dt, int metric, float* qf32, void* qop, float* qeps,
-                               const unsigned* max_sq_bits, const float* mu, double* qxn2, hipStream_t s);
+// search(): query preparation (k_prep_queries): fp32 copy for the exact
+// refine, the scan operand, and the per-query certification terms
+struct PrepParams {
+    const void* q;          // [nq][d] caller queries, dtype q_dt, on the device
+    int q_dt;
+    int64_t nq, nq_pad;
+    int d, kdim;
+    int st_dt;              // scan dtype (F32, BF16, F16, F32S)
+    int metric;
+    float* qf32;            // [nq_pad][kdim] fp32 queries, zero padded
+    void* qop;              // [nq_pad][row_bytes] scan operand (x - mu in the scan dtype, pre-scaled)
+    float* qeps;            // [nq] E
+    float* qrho;            // [nq] rho
+    double* qshift;         // [nq] s_q
+    const unsigned* mbits;     // max |y|^2 of the stored rows (float bits)
+    const unsigned* img_bits;  // max srcC of the scan image (= mbits without an image)
+    const float* mu;        // centre of the scan image (null: none)
+};
+hipError_t launch_prep_queries(const PrepParams& p, hipStream_t s);
 hipError_t launch_scan(int st_dt, int metric, const ScanParams& p, hipStream_t s);
 // fx_scan.hip: the MFMA scan; *handled = false when it has no kernel for p.row_bytes
 hipError_t launch_scan_mfma(int st_dt, int metric, const ScanParams& p, hipStream_t s, bool* handled);
-// fx_scan_q32.hip: the small-batch scan (p.q32_tiles > 0)
-hipError_t launch_scan_q32(int st_dt, int metric, const ScanParams& p, hipStream_t s, bool* handled);
-// fx_scan_w.hip: the wide-tile scan for large batches (p.n_wtiles > 0)
-hipError_t launch_scan_w(int st_dt, int metric, const ScanParams& p, hipStream_t s);
-bool scan_w_supported(int st_dt, int row_bytes);
-int scan_w_queries();
 hipError_t launch_refine(int st_dt, int metric, const RefineParams& p, hipStream_t s);
 // small batches: merge each 16 splits' candidate lists of a query into their
 // top KP (k_reduce_cand); *ngroups = ceil(splits / 16) lists per query after
@@ -153,11 +159,18 @@ hipError_t launch_merge_shards(int metric, int nshards, int64_t nq, int k, const
 // maximum -> cmax_bits (atomicMax)
 hipError_t launch_split_rows(const float* codes, int kdim, int64_t r0, int64_t r1, const float* mu, void* split,
                              float* cnorms, unsigned* cmax_bits, hipStream_t s);
-// mu[kdim] <- mean of a strided sample of <= MU_SAMPLE of the n fp32 rows
-// (part: MU_GROUPS * kdim doubles of scratch)
+// mu[kdim] <- mean of a strided sample of <= MU_SAMPLE of the n stored rows
+// (dtype dt, row stride row_bytes; part: 2 * MU_GROUPS * kdim doubles of
+// scratch).  min_ratio > 0: mu is set to 0 when |mu|^2 < min_ratio * the
+// sample's mean |y|^2 (no common direction to remove)
 constexpr int64_t MU_SAMPLE = 1 << 20;
 constexpr int MU_GROUPS = 64;
-hipError_t launch_mu(const float* codes, int kdim, int d, int64_t n, double* part, float* mu, hipStream_t s);
+hipError_t launch_mu(const char* codes, int dt, int row_bytes, int d, int64_t n, double* part, float* mu,
+                     float min_ratio, hipStream_t s);
+// 16-bit rows [r0, r1) -> cnorms = |y - mu|^2 (fp64 sum, one rounding; mu null:
+// |y|^2), their maximum -> cmax_bits (atomicMax)
+hipError_t launch_centre_norms(const char* codes, int dt, int row_bytes, int64_t r0, int64_t r1, const float* mu,
+                               float* cnorms, unsigned* cmax_bits, hipStream_t s);
 hipError_t launch_synth(void* out, int64_t row0, int64_t n, int d, int dtype, uint64_t seed,
                         hipStream_t s);
 hipError_t launch_to_f32(const void* codes, int st_dt, int row_bytes, int64_t n, int d, float* out,

@@ -293,33 +293,102 @@ __global__ __launch_bounds__(256) void k_convert_rows_t(const void* __restrict__
     if (threadIdx.x == 0 && bmax) atomicMax(max_sq_bits, bmax);
 }
 
-// Centre of the F32S scan image (L2): mu = mean of a strided sample of up to
-// MU_SAMPLE rows.  Any mu gives correct results (distances are translation
-// invariant and the certification margin is computed for the centred
-// operands); a centre inside the data shrinks the operands' norms, and with
-// them the margin, by the spread-to-norm ratio of clustered embeddings.
-// Pass 1: block (column group of 64, row group g) sums its sample rows in fp64;
-// pass 2 sums the row groups in a fixed order (deterministic).
-__global__ __launch_bounds__(256) void k_mu_partial(const float* __restrict__ codes, int kdim, int64_t n,
-                                                    int64_t ns, double* __restrict__ part) {
-    __shared__ double red[4][64];
+// Centre of an L2 scan image: mu = mean of a strided sample of up to
+// MU_SAMPLE stored rows.  Any mu gives correct results (distances are
+// translation invariant and the certification terms are computed for the
+// centred operands); a centre inside the data shrinks the operands' norms,
+// and with them the bound, by the spread-to-norm ratio of clustered
+// embeddings.  Pass 1: block (column group of 64, row group g) sums its sample
+// rows and their squares in fp64; pass 2 (one block) sums the row groups in a
+// fixed order (deterministic) and, when min_ratio > 0, drops a centre whose
+// norm is small next to the rows' (mu = 0: no common direction to remove).
+__global__ __launch_bounds__(256) void k_mu_partial(const char* __restrict__ codes, int dt, int row_bytes, int kdim,
+                                                    int64_t n, int64_t ns, double* __restrict__ part) {
+    __shared__ double red[2][4][64];
     const int c = blockIdx.x * 64 + (threadIdx.x & 63), sub = threadIdx.x >> 6, g = blockIdx.y;
-    double acc = 0.0;
+    double acc = 0.0, acc2 = 0.0;
     if (c < kdim)
-        for (int64_t i = (int64_t)g * 4 + sub; i < ns; i += MU_GROUPS * 4)
-            acc += (double)codes[(i * n / ns) * kdim + c];
-    red[sub][threadIdx.x & 63] = acc;
+        for (int64_t i = (int64_t)g * 4 + sub; i < ns; i += MU_GROUPS * 4) {
+            const double v = (double)load_elem(codes + (i * n / ns) * (int64_t)row_bytes, c, dt);
+            acc += v;
+            acc2 += v * v;
+        }
+    red[0][sub][threadIdx.x & 63] = acc;
+    red[1][sub][threadIdx.x & 63] = acc2;
     __syncthreads();
-    if (sub == 0 && c < kdim)
-        part[(int64_t)g * kdim + c] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    if (sub == 0 && c < kdim) {
+        const int l = threadIdx.x;
+        part[(int64_t)g * kdim + c] = red[0][0][l] + red[0][1][l] + red[0][2][l] + red[0][3][l];
+        part[(int64_t)(MU_GROUPS + g) * kdim + c] = red[1][0][l] + red[1][1][l] + red[1][2][l] + red[1][3][l];
+    }
 }
 __global__ __launch_bounds__(256) void k_mu_finish(const double* __restrict__ part, int kdim, int d, int64_t ns,
-                                                   float* __restrict__ mu) {
-    const int c = blockIdx.x * 256 + threadIdx.x;
-    if (c >= kdim) return;
-    double s = 0.0;
-    for (int g = 0; g < MU_GROUPS; ++g) s += part[(int64_t)g * kdim + c];
-    mu[c] = c < d ? (float)(s / (double)ns) : 0.0f;  // padding columns stay 0
+                                                   float min_ratio, float* __restrict__ mu) {
+    __shared__ double red[2][256];
+    double m2 = 0.0, y2 = 0.0;
+    for (int c = threadIdx.x; c < kdim; c += 256) {
+        double s = 0.0, s2 = 0.0;
+        for (int g = 0; g < MU_GROUPS; ++g) {
+            s += part[(int64_t)g * kdim + c];
+            s2 += part[(int64_t)(MU_GROUPS + g) * kdim + c];
+        }
+        const float m = c < d ? (float)(s / (double)ns) : 0.0f;  // padding columns stay 0
+        mu[c] = m;
+        m2 += (double)m * m;
+        y2 += s2 / (double)ns;
+    }
+    red[0][threadIdx.x] = m2;
+    red[1][threadIdx.x] = y2;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) {
+            red[0][threadIdx.x] += red[0][threadIdx.x + o];
+            red[1][threadIdx.x] += red[1][threadIdx.x + o];
+        }
+        __syncthreads();
+    }
+    if (min_ratio > 0.0f && red[0][0] < (double)min_ratio * red[1][0])
+        for (int c = threadIdx.x; c < kdim; c += 256) mu[c] = 0.0f;
+}
+
+// 16-bit L2 scan image (IMG_C16): per stored row, S = |y - mu|^2 (fp64 sum
+// of the exact differences, one rounding to fp32) -- the scan's srcC, whose
+// query operand is then x - mu -- and its maximum -> cmax_bits.  One wave per
+// row, 16-B chunks per lane, grid-stride.
+template <int DT>
+__global__ __launch_bounds__(256) void k_centre_norms(const char* __restrict__ codes, int row_bytes, int64_t r0,
+                                                      int64_t r1, const float* __restrict__ mu,
+                                                      float* __restrict__ cnorms, unsigned* __restrict__ cmax_bits) {
+    __shared__ unsigned bmax;
+    if (threadIdx.x == 0) bmax = 0u;
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int nchunk = row_bytes / 16;
+    unsigned my_max = 0u;
+    for (int64_t row = r0 + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < r1; row += (int64_t)gridDim.x * 4) {
+        const char* src = codes + row * (int64_t)row_bytes;
+        double acc = 0.0;
+        for (int c = lane; c < nchunk; c += 64) {
+            const cv_u32x4 w4 = __builtin_nontemporal_load((const cv_u32x4*)(src + c * 16));
+            const uint32_t w[4] = {w4[0], w4[1], w4[2], w4[3]};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint16_t hv = (uint16_t)(w[j >> 1] >> (16 * (j & 1)));
+                const double y = (double)(DT == BF16 ? bf2f(hv) : h2f(hv));
+                const double t = y - (mu ? (double)mu[c * 8 + j] : 0.0);
+                acc = fma(t, t, acc);
+            }
+        }
+        acc = wave_sum_f64(acc);
+        if (lane == 0) {
+            const float sq = (float)acc;
+            cnorms[row] = sq;
+            my_max = max(my_max, __float_as_uint(sq));
+        }
+    }
+    if (lane == 0 && my_max) atomicMax(&bmax, my_max);
+    __syncthreads();
+    if (threadIdx.x == 0 && bmax) atomicMax(cmax_bits, bmax);
 }
 
 // fp32 rows -> F32S scan image: row r, v = fl(y - mu) (mu = 0 when null),
@@ -370,73 +439,99 @@ __global__ __launch_bounds__(256) void k_split_rows(const float* __restrict__ co
 // ---------------------------------------------------------------------------
 // search(): query preparation
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_prep_queries(const void* __restrict__ q, int q_dt, int64_t nq,
-                                                      int64_t nq_pad, int d, int kdim, int st_dt, int metric,
-                                                      float* __restrict__ qf32, void* __restrict__ qop,
-                                                      float* __restrict__ qeps, const unsigned* __restrict__ max_sq_bits,
-                                                      const float* __restrict__ mu, double* __restrict__ qxn2,
-                                                      double gamma) {
+// One wave per query row.  Scan operand and certification terms by mode:
+//   F32S (fp32 index, split image): [hi | lo] bf16 planes of -2 (x - mu) (IP:
+//     -x); E from the split scan's dropped terms, shift =
+//     |x - mu|^2, rho = 0;
+//   L2, scan dtype F32 / BF16 / F16: operand -2 op with op = rn_dt(fl(x - mu))
+//     (mu = 0 without a centred image); with r = (x - mu) - op (exact in fp64)
+//     the scan key of row y is  a(y) = srcC - 2 op.y  (srcC = |y - mu|^2, or
+//     |y|^2 without a centre), and  a(y) + s_q = D(y) + 2 r.(y - x) + err,
+//     s_q = |x|^2 - |mu|^2 - 2 r.x,  |2 r.(y - x)| <= 2 rho sqrt(D(y)),
+//     rho = |r|,  |err| <= E = u Smax + gamma_{K+1} (Smax + 2 M |op|)
+//     (fp32 fma-chain accumulation of K exact products onto srcC: Smax = max
+//     srcC, M = max |y|);
+//   IP: operand -op, op = rn_dt(x): a(y) = -x.y + r.y, E = (gamma + u) |op| M
+//     + rho M, shift 0, rho 0.
+// A non-finite operand (fp16 overflow of -2 op) sets E = +inf: the query is
+// never certified and goes to the exact fallback.
+__global__ __launch_bounds__(256) void k_prep_queries(PrepParams p, double gamma) {
     const int lane = threadIdx.x & 63;
     const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (r >= nq_pad) return;
-    const bool live = r < nq;
-    double s = 0.0, sc = 0.0;
-    bool inexact = false;
+    if (r >= p.nq_pad) return;
+    const bool live = r < p.nq;
+    const int kdim = p.kdim;
+    const float scale = p.metric == L2 ? -2.0f : -1.0f;
+    // xn2 |x|^2, sc |x - mu|^2 (F32S), on2 |op|^2, rr |r|^2, rx r.x, mn2 |mu|^2
+    double xn2 = 0.0, sc = 0.0, on2 = 0.0, rr = 0.0, rx = 0.0, mn2 = 0.0;
+    bool bad = false;
     for (int c = lane; c < kdim; c += 64) {
-        float v = (live && c < d) ? load_elem(q, r * d + c, q_dt) : 0.0f;
-        qf32[r * (int64_t)kdim + c] = v;
-        // |x - mu|^2 for the certification (fp64 of the fp32 operands; mu = 0
-        // unless the F32S image is centred)
-        const double xm = (double)v - (mu ? (double)mu[c] : 0.0);
-        sc += xm * xm;
-        if (st_dt == F32S) {
-            // split scan operand [hi plane | lo plane] of the pre-scaled
-            // (centred) query (x' - hi is exact in fp32: hi is within 2^-8 |x'|
-            // of x')
-            const float vc = mu ? v - mu[c] : v;
-            s += (double)vc * (double)vc;
-            const float xs = vc * (metric == L2 ? -2.0f : -1.0f);
+        const float v = (live && c < p.d) ? load_elem(p.q, r * p.d + c, p.q_dt) : 0.0f;
+        p.qf32[r * (int64_t)kdim + c] = v;
+        const float m = p.mu ? p.mu[c] : 0.0f;
+        xn2 += (double)v * (double)v;
+        mn2 += (double)m * (double)m;
+        if (p.st_dt == F32S) {
+            // split operand of the pre-scaled (centred) query (x' - hi is exact
+            // in fp32: hi is within 2^-8 |x'| of x')
+            const float vc = v - m;
+            const double xm = (double)v - (double)m;
+            sc += xm * xm;
+            on2 += (double)vc * (double)vc;
+            const float xs = vc * scale;
             const uint16_t hi = f2bf(xs);
-            uint16_t* row = (uint16_t*)qop + r * (int64_t)(2 * kdim);
+            uint16_t* row = (uint16_t*)p.qop + r * (int64_t)(2 * kdim);
             row[c] = hi;
             row[kdim + c] = f2bf(xs - bf2f(hi));
         } else {
-            // scan operand: x rounded to the storage dtype, pre-scaled (exactly,
-            // by a power of two) so that the MFMA accumulator is the key:
-            // L2: acc = -2 x.y (+ |y|^2 from the accumulator init); IP: -x.y
-            const float st = round_to(v, st_dt);
-            inexact |= st != v;
-            store_elem(qop, r * (int64_t)kdim + c, st_dt, st * (metric == L2 ? -2.0f : -1.0f));
-            s += (double)v * (double)v;
+            const float op = round_to(v - m, p.st_dt);
+            const float sop = op * scale;  // exact (power of two) unless it overflows fp16
+            bad |= !__builtin_isfinite(round_to(sop, p.st_dt));
+            store_elem(p.qop, r * (int64_t)kdim + c, p.st_dt, sop);
+            const double rc = ((double)v - (double)m) - (double)op;
+            rr += rc * rc;
+            rx += rc * (double)v;
+            on2 += (double)op * (double)op;
         }
     }
-    s = wave_sum_f64(s);
+    xn2 = wave_sum_f64(xn2);
     sc = wave_sum_f64(sc);
-    if (live && lane == 0) qxn2[r] = sc;
-    inexact = __any(inexact);
-    if (live && lane == 0) {
-        // Worst-case bound on |approx - exact| of the scan's key for any row
-        // (DESIGN.md "certification"): fp32 fma-chain dot and |y|^2 over K =
-        // kdim terms (gamma = K u / (1 - K u)), one more rounding in the key
-        // (u), and the query's rounding to the storage dtype (delta).
-        const double u = 5.9604644775390625e-8;  // 2^-24
-        // M = the largest row norm of the scanned operand (stored rows, or
-        // the centred F32S image), read on the device (add() never waits for
-        // the host to learn it); xn = the scanned query's norm
-        const double xn = sqrt(s), M = sqrt((double)__uint_as_float(*max_sq_bits));
-        // F32S: the split scan drops lo*lo and both residuals v - hi - lo;
-        // per product <= 3 * 2^-16 (1 + 2^-7) |x_k||y_k|;
-        // gamma then covers its 3 K products (launch_prep_queries)
-        const double delta = st_dt == F32S ? 4.73e-5
-                                           : (inexact ? (st_dt == BF16 ? 3.90625e-3 : 4.8828125e-4) : 0.0);
-        // centring (F32S): the operands are fl(y - mu), fl(x - mu): each
-        // product and square carries <= 2u + u^2 more (3u covers it)
-        const double cu = mu ? 3.0 * u : 0.0;
-        double eps;
-        if (metric == L2) eps = (2.0 * gamma + u + cu) * (M * M + 2.0 * xn * M) + 2.0 * delta * xn * M;
-        else eps = (gamma + u) * xn * M + delta * xn * M;
-        qeps[r] = (float)(eps * 1.0625 + 1e-30);
+    on2 = wave_sum_f64(on2);
+    rr = wave_sum_f64(rr);
+    rx = wave_sum_f64(rx);
+    mn2 = wave_sum_f64(mn2);
+    bad = __any(bad);
+    if (!live || lane != 0) return;
+    const double u = 5.9604644775390625e-8;  // 2^-24
+    // M: the largest stored-row norm; Smax: the largest srcC of the scan image
+    // (both read on the device: add() never waits for the host to learn them)
+    const double M = sqrt((double)__uint_as_float(*p.mbits));
+    const double Smax = (double)__uint_as_float(*p.img_bits);
+    const double on = sqrt(on2);
+    double eps, shift = 0.0, rho = 0.0;
+    if (p.st_dt == F32S) {
+        // the split scan drops lo*lo and both residuals v - hi - lo: per
+        // product <= 3 * 2^-16 (1 + 2^-7) |x_k||y_k| (delta); centring: the
+        // operands are fl(y - mu), fl(x - mu): each product and square carries
+        // <= 2u + u^2 more (3u); gamma covers its 3 K + 1 accumulated terms
+        const double Mc = sqrt(Smax), delta = 4.73e-5, cu = p.mu ? 3.0 * u : 0.0;
+        if (p.metric == L2) {
+            eps = (2.0 * gamma + u + cu) * (Mc * Mc + 2.0 * on * Mc) + 2.0 * delta * on * Mc;
+            shift = sc;
+        } else {
+            eps = (gamma + u) * on * Mc + delta * on * Mc;
+        }
+    } else if (p.metric == L2) {
+        eps = u * Smax * 1.01 + gamma * (Smax * 1.01 + 2.0 * M * on);
+        shift = xn2 - mn2 - 2.0 * rx;
+        eps += 1e-12 * (xn2 + mn2 + 2.0 * fabs(rx));  // fp64 rounding of shift
+        rho = sqrt(rr);
+    } else {
+        eps = (gamma + u) * on * M + sqrt(rr) * M;
     }
+    p.qeps[r] = bad ? FX_INF : (float)(eps * 1.0625 + 1e-30);
+    p.qrho[r] = (float)(rho * 1.0000002);
+    p.qshift[r] = shift;
 }
 
 // ---------------------------------------------------------------------------
@@ -766,6 +861,25 @@ hipError_t launch_reduce_cand(const float* cd, const int* ci, int splits, int64_
     return hipGetLastError();
 }
 
+// Certification of a query's top-k: every row the selection
+// dropped has approx key >= tb, so (k_prep_queries) its exact distance D
+// satisfies D + 2 rho sqrt(D) >= T = tb + shift - E, i.e.
+// sqrt(D) >= sqrt(rho^2 + T) - rho = T / (sqrt(rho^2 + T) + rho) (rho = 0:
+// D >= T, which is also the IP form).  The top-k is exact when the k-th
+// exact key, plus 2 ulp for its own fp32 rounding, lies below that.
+__device__ __forceinline__ bool certified(float kth, float tb, const RefineParams& p, int64_t q) {
+    const double T = (double)tb + p.qshift[q] - (double)p.qeps[q];
+    const double rho = (double)p.qrho[q];
+    double dmin = T;
+    if (rho > 0.0) {
+        const double t = T > 0.0 ? T : 0.0;
+        const double sd = t / (sqrt(rho * rho + t) + rho);
+        dmin = sd * sd * (1.0 - 1e-12);
+    }
+    const double kup = (double)kth + fabs((double)kth) * 2.384185791015625e-7;  // + 2 ulp
+    return kup < dmin;
+}
+
 // PF = chunks of 64 candidates whose loads are issued together in phase 1
 // (PF = 4 for the small-batch scan's many splits: one wave per query is
 // latency-bound on one dependent load per chunk otherwise)
@@ -836,8 +950,6 @@ __global__ __launch_bounds__(256) void k_refine(RefineParams p) {
         const double v = __shfl(a, (lane & 3) * 16, 64);
         if ((lane >> 2) == r) ex = v;
     }
-    // |x - mu|^2 (mu: the scan image's centre, 0 if none), from k_prep_queries
-    const double xn2 = METRIC == L2 ? p.qxn2[q] : 0.0;
 
     // ---- phase 3: order by (fp32 exact key, id), write top-k, certify
     float key = FX_INF;
@@ -860,9 +972,7 @@ __global__ __launch_bounds__(256) void k_refine(RefineParams p) {
         // a split may also have pruned with the shared threshold (a bound on
         // a rank below KP, compact_wave): dropped rows lie above min(td, it)
         const float tb = p.gtau ? fminf(td, ord2f(p.gtau[q])) : td;
-        const double bound = (METRIC == L2 ? (double)tb + xn2 : (double)tb) - (double)p.qeps[q];
-        const double kup = (double)kth + fabs((double)kth) * 2.384185791015625e-7;  // + 2 ulp
-        if (!(kup < bound) && lane == 0 && !p.force_fb) {
+        if (!certified(kth, tb, p, q) && lane == 0 && !p.force_fb) {
             const int pos = atomicAdd(p.n_flag, 1);
             p.flag_list[pos] = (int)q;
         }
@@ -944,7 +1054,6 @@ __global__ __launch_bounds__(BT_THREADS) void k_refine_big(RefineParams p) {
         ei[t] = INT_MAX;
     }
     bt_sort(ed, ei, n2);  // (syncs: ed/ei complete)
-    const double xn2 = METRIC == L2 ? p.qxn2[q] : 0.0;  // |x - mu|^2 (k_prep_queries)
 
     // phase 3: top-k out (faiss padding past the candidates), certification
     for (int t = tid; t < p.k; t += BT_THREADS) {
@@ -957,10 +1066,7 @@ __global__ __launch_bounds__(BT_THREADS) void k_refine_big(RefineParams p) {
         if (!(tb < FX_INF)) ok = true;  // no row was dropped anywhere: the candidates are every row
         else if (n1 < p.k) ok = false;
         else {
-            const float kth = ed[p.k - 1];
-            const double bound = (METRIC == L2 ? (double)tb + xn2 : (double)tb) - (double)p.qeps[q];
-            const double kup = (double)kth + fabs((double)kth) * 2.384185791015625e-7;  // + 2 ulp
-            ok = kup < bound;
+            ok = certified(ed[p.k - 1], tb, p, q);
         }
         if (!ok || p.force_fb) {
             const int pos = atomicAdd(p.n_flag, 1);
@@ -1175,43 +1281,24 @@ hipError_t launch_convert_rows(const void* x, int x_dt, int64_t n, int d, void* 
     const int nchunk = kdim / (st_dt == F32 ? 4 : 8);
     int R = 1;
     while (R < 4 && (R * nchunk) % 64 != 0) R *= 2;
-    // FX_CONVERT_WIDE=1: twice the rows per wave iteration (up to 8 chunks in
-    // flight per lane)
-    static const bool wide = getenv("FX_CONVERT_WIDE") && atoi(getenv("FX_CONVERT_WIDE")) == 1;
-    const int cpl = wide && (R * nchunk) % 64 == 0 && 2 * R * nchunk <= 512 ? 8 : 4;
-    if (cpl == 8) R *= 2;
-    if (vec && R * nchunk <= 64 * cpl && !getenv("FX_CONVERT_V1")) {
+    if (vec && R * nchunk <= 64 * 4) {
         // grid-stride over row groups with a bounded grid (ROWS_GRID_CAP);
-        // FX_CONVERT_GRID overrides the cap (A/B runs)
-        static const int gcap =
-            getenv("FX_CONVERT_GRID") ? std::max(1, atoi(getenv("FX_CONVERT_GRID"))) : ROWS_GRID_CAP;
-        const unsigned grid = grid_for((n + R - 1) / R, 4, gcap);
-        // nontemporal loads / stores by default (1M x 768 bf16: 0.900 -> 0.882 ms,
-        // same box); FX_CONVERT_NT=0: cached ones
-        static const bool nt = !(getenv("FX_CONVERT_NT") && atoi(getenv("FX_CONVERT_NT")) == 0);
-#define FX_CONV_NT(XD, SD, NT, C)                                                                                 \
-            if (normalize)                                                                                       \
-                hipLaunchKernelGGL((k_convert_rows_t<XD, SD, true, NT, C>), dim3(grid), dim3(256), 0, s, x, n,   \
-                                   d, codes_row0, kdim, norms_row0, max_sq_bits, R);                            \
-            else                                                                                                 \
-                hipLaunchKernelGGL((k_convert_rows_t<XD, SD, false, NT, C>), dim3(grid), dim3(256), 0, s, x, n,  \
-                                   d, codes_row0, kdim, norms_row0, max_sq_bits, R);
+        // nontemporal loads / stores (1M x 768 bf16: 0.900 -> 0.882 ms, same box)
+        const unsigned grid = grid_for((n + R - 1) / R, 4, ROWS_GRID_CAP);
 #define FX_CONV(XD, SD)                                                                                           \
         if (x_dt == XD && st_dt == SD) {                                                                         \
-            if (cpl == 8) {                                                                                      \
-                FX_CONV_NT(XD, SD, true, 8)                                                                      \
-            } else if (nt) {                                                                                     \
-                FX_CONV_NT(XD, SD, true, 4)                                                                      \
-            } else {                                                                                             \
-                FX_CONV_NT(XD, SD, false, 4)                                                                     \
-            }                                                                                                    \
+            if (normalize)                                                                                       \
+                hipLaunchKernelGGL((k_convert_rows_t<XD, SD, true, true, 4>), dim3(grid), dim3(256), 0, s, x, n, \
+                                   d, codes_row0, kdim, norms_row0, max_sq_bits, R);                            \
+            else                                                                                                 \
+                hipLaunchKernelGGL((k_convert_rows_t<XD, SD, false, true, 4>), dim3(grid), dim3(256), 0, s, x,   \
+                                   n, d, codes_row0, kdim, norms_row0, max_sq_bits, R);                         \
             return hipGetLastError();                                                                            \
         }
         FX_CONV(F32, F32) FX_CONV(F32, BF16) FX_CONV(F32, F16)
         FX_CONV(BF16, F32) FX_CONV(BF16, BF16) FX_CONV(BF16, F16)
         FX_CONV(F16, F32) FX_CONV(F16, BF16) FX_CONV(F16, F16)
 #undef FX_CONV
-#undef FX_CONV_NT
     }
     hipLaunchKernelGGL(k_convert_rows, dim3(grid_for(n, 4, ROWS_GRID_CAP)), dim3(256), 0, s, x, x_dt, n, d, codes_row0,
                        st_dt, kdim, norms_row0, max_sq_bits, normalize, vec);
@@ -1226,24 +1313,36 @@ hipError_t launch_split_rows(const float* codes, int kdim, int64_t r0, int64_t r
     return hipGetLastError();
 }
 
-hipError_t launch_mu(const float* codes, int kdim, int d, int64_t n, double* part, float* mu, hipStream_t s) {
+hipError_t launch_mu(const char* codes, int dt, int row_bytes, int d, int64_t n, double* part, float* mu,
+                     float min_ratio, hipStream_t s) {
     if (n <= 0) return hipErrorInvalidValue;
+    const int kdim = row_bytes / dtype_size(dt);
     const int64_t ns = n < MU_SAMPLE ? n : MU_SAMPLE;
-    hipLaunchKernelGGL(k_mu_partial, dim3((unsigned)((kdim + 63) / 64), MU_GROUPS), dim3(256), 0, s, codes, kdim, n,
-                       ns, part);
-    hipLaunchKernelGGL(k_mu_finish, dim3((unsigned)((kdim + 255) / 256)), dim3(256), 0, s, part, kdim, d, ns, mu);
+    hipLaunchKernelGGL(k_mu_partial, dim3((unsigned)((kdim + 63) / 64), MU_GROUPS), dim3(256), 0, s, codes, dt,
+                       row_bytes, kdim, n, ns, part);
+    hipLaunchKernelGGL(k_mu_finish, dim3(1), dim3(256), 0, s, part, kdim, d, ns, min_ratio, mu);
     return hipGetLastError();
 }
 
-hipError_t launch_prep_queries(const void* q, int q_dt, int64_t nq, int64_t nq_pad, int d, int kdim, int st_dt,
-                               int metric, float* qf32, void* qop, float* qeps, const unsigned* max_sq_bits,
-                               const float* mu, double* qxn2, hipStream_t s) {
+hipError_t launch_centre_norms(const char* codes, int dt, int row_bytes, int64_t r0, int64_t r1, const float* mu,
+                               float* cnorms, unsigned* cmax_bits, hipStream_t s) {
+    if (r1 <= r0) return hipSuccess;
+    const dim3 g(grid_for(r1 - r0, 4, ROWS_GRID_CAP));
+    if (dt == BF16)
+        hipLaunchKernelGGL(k_centre_norms<BF16>, g, dim3(256), 0, s, codes, row_bytes, r0, r1, mu, cnorms, cmax_bits);
+    else if (dt == F16)
+        hipLaunchKernelGGL(k_centre_norms<F16>, g, dim3(256), 0, s, codes, row_bytes, r0, r1, mu, cnorms, cmax_bits);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+hipError_t launch_prep_queries(const PrepParams& p, hipStream_t s) {
     const double u = 5.9604644775390625e-8;
     // terms accumulated by the scan's fp32 MFMA chain: K products (3 K for F32S) + srcC
-    const double nt = st_dt == F32S ? 3.0 * kdim + 1.0 : (double)kdim;
+    const double nt = p.st_dt == F32S ? 3.0 * p.kdim + 1.0 : (double)p.kdim + 1.0;
     const double gamma = nt * u / (1.0 - nt * u);
-    hipLaunchKernelGGL(k_prep_queries, dim3((unsigned)((nq_pad + 3) / 4)), dim3(256), 0, s, q, q_dt, nq, nq_pad, d,
-                       kdim, st_dt, metric, qf32, qop, qeps, max_sq_bits, mu, qxn2, gamma);
+    hipLaunchKernelGGL(k_prep_queries, dim3((unsigned)((p.nq_pad + 3) / 4)), dim3(256), 0, s, p, gamma);
     return hipGetLastError();
 }
 
@@ -1260,18 +1359,12 @@ static hipError_t scan_t(const ScanParams& p, hipStream_t s) {
 hipError_t launch_scan(int st_dt, int metric, const ScanParams& p, hipStream_t s) {
     // the MFMA scan (fx_scan.hip) covers every row width it has a register
     // layout for; other widths take the generic kernel above
-    if (p.n_wtiles > 0) return launch_scan_w(st_dt, metric, p, s);  // wide tiles (fx_scan_w.hip)
-    if (p.q32_tiles > 0) {  // small batch: k_scan_q32 (fx_scan_q32.hip); the host planned for it
-        bool handled = false;
-        hipError_t e = launch_scan_q32(st_dt, metric, p, s, &handled);
-        return handled ? e : hipErrorInvalidValue;
-    }
     if (st_dt == F32S) {  // the split-fp32 operand exists only for the MFMA scans
         bool handled = false;
         hipError_t e = launch_scan_mfma(st_dt, metric, p, s, &handled);
         return handled ? e : hipErrorInvalidValue;
     }
-    if (!getenv("FX_SCAN_V1")) {
+    {
         bool handled = false;
         hipError_t e = launch_scan_mfma(st_dt, metric, p, s, &handled);
         if (handled) return e;

@@ -458,13 +458,14 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                     static_for<M>([&](auto MM) {
                         constexpr int m = decltype(MM)::value;
                         const unsigned el = (pn >> (4 * m)) & 15u;
-                        if (__builtin_amdgcn_ballot_w64(el != 0u))
+                        if (__builtin_amdgcn_ballot_w64(el != 0u)) {
                             if constexpr (FX_V4_ATOMPUSH)
                                 ovf |= push_group<M, N>(acc, n, m, el, tq, qloc[n], trow0 + rl0 + m * 16, rlim, lst_d,
                                                         lst_i, cnt, pend[n]);
                             else
                                 ovf |= push_lean<M, N>(acc, n, m, el, tq, qloc[n], trow0 + rl0 + m * 16, rlim, ld_off,
                                                        li_off, trash, cnt, pend[n]);
+                        }
                     });
                 });
             }
@@ -512,14 +513,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
     }
 }
 
-template <int DT, int METRIC, int KSTEPS, int ABL = 0, int LN = 0>
+template <int DT, int METRIC, int KSTEPS, int ABL = 0, int LN = 1>
 static hipError_t scan_v4_t(const ScanParams& p, hipStream_t s) {
-    // full-line pieces are the default; FX_SCAN_LINE=0 selects the
-    // fragment-shaped pieces of round 1 (A/B only)
-    if constexpr (ABL == 0 && LN == 0) {
-        static const int ln = getenv("FX_SCAN_LINE") ? atoi(getenv("FX_SCAN_LINE")) : 1;
-        if (ln != 0) return scan_v4_t<DT, METRIC, KSTEPS, 0, 1>(p, s);
-    }
 #ifdef FX_ABLATION
     if constexpr (ABL == 0 && DT == BF16 && METRIC == L2 && KSTEPS == 24) {
         switch (p.dbg & 511) {

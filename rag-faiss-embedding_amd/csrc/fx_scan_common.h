@@ -1,5 +1,5 @@
 // fx_scan_common.h -- device helpers shared by the MFMA scan kernels
-// (fx_scan.hip: k_scan_v4; fx_scan_q32.hip: k_scan_q32):
+// (fx_scan.hip: k_scan_v4):
 // LDS-DMA pieces with scalar bases, pinned LDS->operand reads, per-wave
 // candidate lists.
 #pragma once

@@ -200,6 +200,11 @@ class _FlatIndex:
     def set_id_offset(self, offset: int) -> None:
         check(lib.fx_index_set_id_offset(self._h, int(offset)))
 
+    def set_option(self, name: str, value: int) -> None:
+        """Per-index tuning / diagnostic option (include/fx_index.h
+        ``fx_index_set_option``; defaults from the FX_* environment at creation)."""
+        check(lib.fx_index_set_option(self._h, name.encode(), int(value)))
+
     # -- profiling (bench roofline) -------------------------------------------------
     def profile(self, enable: bool = True) -> None:
         check(lib.fx_index_profile(self._h, 1 if enable else 0))

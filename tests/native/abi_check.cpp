@@ -149,7 +149,8 @@ int main() {
     }
 
     // ---- graph-replayed small host search ---------------------------------
-    setenv("FX_SEARCH_GRAPH", "1", 1);
+    OK(fx_index_set_option(ix, "search_graph", 1));
+    CHECK(fx_index_set_option(ix, "no_such_option", 1) == FX_E_ARG, "unknown option rejected");
     for (int rep = 0; rep < 3; ++rep) search_and_check(ix, xb, n, d, 1, 5, rng, "graph nq=1");
     std::vector<float> extra((size_t)5 * d);
     for (auto& v : extra) v = nd(rng);
@@ -157,7 +158,7 @@ int main() {
     xb.insert(xb.end(), extra.begin(), extra.end());
     n += 5;
     search_and_check(ix, xb, n, d, 1, 5, rng, "graph after add");
-    unsetenv("FX_SEARCH_GRAPH");
+    OK(fx_index_set_option(ix, "search_graph", 0));
 
     // ---- IxF2 round trip, fp32 and bf16 storage ---------------------------
     const std::string path = std::string(getenv("TMPDIR") ? getenv("TMPDIR") : "/tmp") + "/fx_abi_check.bin";

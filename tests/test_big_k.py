@@ -103,7 +103,7 @@ def test_forced_fallback_is_exact(fx, gauss, monkeypatch, k):
     xb, xq = gauss
     ix = fx.IndexFlatL2(384)
     ix.add(xb[:100_000])
-    monkeypatch.setenv("FX_FORCE_FALLBACK", "1")
+    ix.set_option("force_fallback", 1)
     D, I = ix.search(xq, k)
     assert ix.last_fallbacks() == len(xq)
     Dr, Ir = C.knn_exact(xq, xb[:100_000], k)
@@ -118,7 +118,7 @@ def test_forced_fallback_many_queries(fx, monkeypatch):
     xq = rng.standard_normal((5000, 64)).astype(np.float32)
     ix = fx.IndexFlatL2(64)
     ix.add(xb)
-    monkeypatch.setenv("FX_FORCE_FALLBACK", "1")
+    ix.set_option("force_fallback", 1)
     D, I = ix.search(xq, 7)
     assert ix.last_fallbacks() == 5000
     Dr, Ir = C.knn_exact(xq, xb, 7)

@@ -7,8 +7,7 @@ time.  Here the issue order of every kernel is replayed per wave and each
 wait is checked to retire exactly the stages it must, for every stage count
 per tile the kernels instantiate.
 
-Formulas restated from fx_scan.hip (k_scan_v4) and fx_scan_q32.hip
-(k_scan_q32: same issue order as k_scan_v4).
+Formulas restated from fx_scan.hip (k_scan_v4).
 """
 import pytest
 
@@ -46,7 +45,7 @@ def _replay(spt, pieces, aux_first, pro_wait, loop_wait, tiles=4):
 
 
 @pytest.mark.parametrize("ksteps", [8, 12, 16, 24])
-def test_v4_and_q32_waits(ksteps):
+def test_v4_waits(ksteps):
     spt = ksteps // 2
     # prologue: vmcnt(12); loop: W = 8 + ((j+3)%SPT==0) + ((j+2)%SPT==0)
     _replay(spt, 4, True, 12, lambda j: 8 + ((j + 3) % spt == 0) + ((j + 2) % spt == 0))

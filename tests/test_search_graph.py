@@ -23,10 +23,8 @@ def fx():
     return faiss
 
 
-@pytest.mark.parametrize("q32", ["0", "1"])
-def test_graph_replay_matches_oracle(fx, monkeypatch, q32):
+def test_graph_replay_matches_oracle(fx, monkeypatch):
     monkeypatch.setenv("FX_SEARCH_GRAPH", "1")
-    monkeypatch.setenv("FX_SCAN_Q32", q32)
     rng = np.random.default_rng(11)
     xb = rng.standard_normal((20_000, 384)).astype(np.float32)
     ix = fx.IndexFlatL2(384)

@@ -13,8 +13,15 @@ One step = one search of one 10k-query batch (queries already resident in
 HBM; results left in HBM).  Corpus and queries are synthetic (counter-hash
 generator shared with oracle/flat_l2.c, exact in bf16), generated on the GPU.
 
-Launch: python bench.py [--gpus 1 --steps 10 --warmup 2]   (N=1)
+Launch: python bench.py [--gpus N --steps 10 --warmup 2]
+          N > 1 without WORLD_SIZE: this process starts N ranks itself
+          (torch.distributed.run, 127.0.0.1) before touching the GPU and
+          passes rank 0's line through;
         python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+          (WORLD_SIZE must equal --gpus).
+--data clustered: a clustered corpus (unit-norm rows around one common
+direction, the shape of sentence embeddings) with fp32 queries that are NOT
+exact in the storage dtype -- the certification's hard case.
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -22,6 +29,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import tempfile
 import time
@@ -30,12 +39,9 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
-import torch  # noqa: E402  (before the HIP library: one runtime per process)
-import torch.distributed as dist  # noqa: E402
-
-import amd_fx  # noqa: E402,F401
-from rag_faiss_embedding_amd import faiss as fx  # noqa: E402
-from rag_faiss_embedding_amd.sharded import ShardedIndexFlatL2, shard_bounds  # noqa: E402
+# torch, torch.distributed and the HIP library are imported in main(), after
+# the launcher decision: a process that starts the ranks never touches the GPU
+torch = dist = fx = None
 
 METRIC = "queries/sec + recall@10 vs CPU FAISS, 10M×768 flat index, 1/2/4/8 MI355X"
 CORPUS_SEED, QUERY_SEED = 1234, 4321
@@ -50,7 +56,6 @@ CONFIGS = {
 # oracle allows; the full-corpus streaming oracle costs ~0.25 s per query on (d)
 # and ~1.2 s on (e) with 16 host cores)
 RECALL_QUERIES = {"d": 256, "b": 1000, "e": 32}
-TORCH_DT = {"float32": torch.float32, "bfloat16": torch.bfloat16, "float16": torch.float16}
 SHORT_DT = {"float32": "f32", "bfloat16": "bf16", "float16": "f16"}
 # MI355X_MICROARCH.md: dense MFMA peaks (TFLOP/s) and HBM3E peak (GB/s)
 MFMA_PEAK = {"float32": 157.3, "bfloat16": 2500.0, "float16": 2500.0}
@@ -61,19 +66,97 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def build_shard(ix, rank, world, n_total, d, dtype, device):
+def launch_plan(gpus: int, env) -> str:
+    """How to run `bench.py --gpus N`: "inproc" (N = 1, or already one rank of
+    a launched world of N), "spawn" (N > 1 and no WORLD_SIZE: start the ranks
+    here), or an error message (WORLD_SIZE set and != N)."""
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return "spawn" if gpus > 1 else "inproc"
+    if int(ws) != gpus:
+        return f"error: WORLD_SIZE={ws} but --gpus {gpus}"
+    return "inproc"
+
+
+def rank_command(gpus: int, argv, port: int):
+    """The torch.distributed.run command that starts one bench rank per GPU."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve())] + list(argv)
+
+
+def spawn_ranks(gpus: int, argv) -> int:
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    log(f"[bench] starting {gpus} ranks (torch.distributed.run, port {port})")
+    return subprocess.call(rank_command(gpus, argv, port), env=env)
+
+
+def torch_dt(dtype):
+    return {"float32": torch.float32, "bfloat16": torch.bfloat16, "float16": torch.float16}[dtype]
+
+
+CLUSTER_SEED, CLUSTER_SPREAD, CLUSTER_CHUNK = 7, 0.1, 1 << 20
+
+
+def clustered_rows(chunk_id: int, nrows: int, d: int, device, base):
+    """Rows of corpus chunk `chunk_id` (CLUSTER_CHUNK rows each) of the
+    clustered corpus: unit-norm base + spread * N(0, I/d), fp32, generated on
+    the GPU from a per-chunk seed (every rank regenerates the same rows)."""
+    g = torch.Generator(device=device).manual_seed(CLUSTER_SEED * 1_000_003 + 1 + chunk_id)
+    x = base[None, :] + CLUSTER_SPREAD * torch.randn((nrows, d), device=device, generator=g) / d ** 0.5
+    return x / x.norm(dim=1, keepdim=True)
+
+
+def clustered_base(d, device):
+    g = torch.Generator(device=device).manual_seed(CLUSTER_SEED)
+    b = torch.randn(d, device=device, generator=g)
+    return b / b.norm()
+
+
+def build_shard(ix, rank, world, n_total, d, dtype, device, data):
     lo, hi = shard_bounds(n_total, world, rank)
     ix.reserve(hi - lo)
     chunk = 1 << 20
-    buf = torch.empty((min(chunk, hi - lo), d), dtype=TORCH_DT[dtype], device=device)
-    for r0 in range(lo, hi, chunk):
-        nr = min(chunk, hi - r0)
-        part = buf[:nr]
-        fx.synth_fill(part, r0, CORPUS_SEED)
-        ix.add(part)
+    if data == "clustered":
+        base = clustered_base(d, device)
+        for c0 in range(lo // CLUSTER_CHUNK * CLUSTER_CHUNK, hi, CLUSTER_CHUNK):
+            rows = clustered_rows(c0 // CLUSTER_CHUNK, min(CLUSTER_CHUNK, n_total - c0), d, device, base)
+            a, b = max(lo, c0), min(hi, c0 + rows.shape[0])
+            ix.add(rows[a - c0:b - c0])
+            del rows
+    else:
+        buf = torch.empty((min(chunk, hi - lo), d), dtype=torch_dt(dtype), device=device)
+        for r0 in range(lo, hi, chunk):
+            nr = min(chunk, hi - r0)
+            part = buf[:nr]
+            fx.synth_fill(part, r0, CORPUS_SEED)
+            ix.add(part)
     ix.set_id_offset(lo)
     torch.cuda.synchronize()
     return lo, hi
+
+
+def make_queries(nq, d, dtype, device, data):
+    if data == "clustered":  # fp32 queries of the same distribution (not exact in 16 bits)
+        g = torch.Generator(device=device).manual_seed(CLUSTER_SEED * 1_000_003)
+        x = clustered_base(d, device)[None, :] + CLUSTER_SPREAD * torch.randn((nq, d), device=device,
+                                                                             generator=g) / d ** 0.5
+        return (x / x.norm(dim=1, keepdim=True)).contiguous()
+    xq = torch.empty((nq, d), dtype=torch_dt(dtype), device=device)
+    fx.synth_fill(xq, 0, QUERY_SEED)
+    return xq
+
+
+def shard_bounds(n_total, world, rank):  # == rag_faiss_embedding_amd.sharded.shard_bounds
+    return n_total * rank // world, n_total * (rank + 1) // world
+
+
+def ShardedIndexFlatL2(*a, **kw):
+    from rag_faiss_embedding_amd.sharded import ShardedIndexFlatL2 as S
+    return S(*a, **kw)
 
 
 def one_step(six, xq, k):
@@ -95,21 +178,41 @@ def oracle_lib_native():
         return C, C.load(), "-march=x86-64-v3"
 
 
-def cpu_baseline_and_recall(args, n_total, d, k, D, I, nthreads):
+def oracle_corpus_chunks(args, n_total, d, dtype, device, rows=None):
+    """(row0, fp32 rows as stored) chunks of the clustered corpus for the CPU
+    oracle, regenerated on this GPU and rounded to the storage dtype."""
+    base = clustered_base(d, device)
+    end = n_total if rows is None else min(rows, n_total)
+    for c0 in range(0, end, CLUSTER_CHUNK):
+        x = clustered_rows(c0 // CLUSTER_CHUNK, min(CLUSTER_CHUNK, n_total - c0), d, device, base)
+        x = x[:end - c0].to(torch_dt(dtype)).float().cpu().numpy()
+        yield c0, x
+
+
+def cpu_baseline_and_recall(args, n_total, d, dtype, k, D, I, xq_dev, nthreads, device):
     """cpu_baseline leg (rank 0): the repo's C/OpenMP restatement of FAISS's
     IndexFlatL2 BLAS path timed on a bounded sample of the same workload, and
     recall@10 of the GPU result against the exact CPU oracle on a query
     sample over the FULL corpus."""
     import numpy as np
+    from oracle import flat_l2 as F
     C, lib, march = oracle_lib_native()
     res = {}
-    # recall: exact streaming oracle (rows regenerated on the fly) vs GPU ids
+    # recall: exact oracle over the full corpus (rows regenerated on the fly) vs GPU ids
     nr = min(args.recall_queries, D.shape[0])
     qsel = np.linspace(0, D.shape[0] - 1, nr).astype(np.int64)
-    from oracle import flat_l2 as F
-    xq = np.concatenate([F.synth(QUERY_SEED, int(q), 1, d) for q in qsel])
     t0 = time.time()
-    Dr, Ir = C.knn_exact_synth(CORPUS_SEED, n_total, d, xq, k, nthreads)
+    if args.data == "clustered":
+        xq = xq_dev[torch.from_numpy(qsel).to(xq_dev.device)].float().cpu().numpy()
+        Ds, Is = [], []
+        for c0, xb in oracle_corpus_chunks(args, n_total, d, dtype, device):
+            Dc, Ic = C.knn_exact(xq, xb, k, nthreads)
+            Ds.append(Dc)
+            Is.append(np.where(Ic >= 0, Ic + c0, -1))
+        Dr, Ir = F.merge_topk(Ds, Is, k)
+    else:
+        xq = np.concatenate([F.synth(QUERY_SEED, int(q), 1, d) for q in qsel])
+        Dr, Ir = C.knn_exact_synth(CORPUS_SEED, n_total, d, xq, k, nthreads)
     t_rec = time.time() - t0
     Ig = I[qsel].cpu().numpy()
     Dgpu = D[qsel].cpu().numpy()
@@ -120,16 +223,25 @@ def cpu_baseline_and_recall(args, n_total, d, k, D, I, nthreads):
     res["recall_sample"] = f"{nr} queries x full {n_total}-row corpus, exact CPU oracle ({t_rec:.1f}s)"
     # timed baseline: BLAS-path port on a corpus slice, extrapolated to n_total
     rows = min(n_total, args.cpu_rows)
-    xb = C.synth(CORPUS_SEED, 0, rows, d, nthreads)
+    if args.data == "clustered":
+        xb = np.concatenate([x for _, x in oracle_corpus_chunks(args, n_total, d, dtype, device, rows)])
+        xall = xq_dev.float().cpu().numpy()
+        xcal, xpool = xall[:128], xall
+    else:
+        xb = C.synth(CORPUS_SEED, 0, rows, d, nthreads)
+        xcal, xpool = C.synth(QUERY_SEED, 0, 128, d, nthreads), None
     # size the timed sample to ~args.cpu_seconds of CPU work (calibrated)
-    xcal = C.synth(QUERY_SEED, 0, 128, d, nthreads)
     t0 = time.time()
     C.knn_blas(xcal, xb, k, nthreads, lib=lib)
     tcal = max(time.time() - t0, 1e-3)
     nq_s = int(min(50_000, max(128, 128 * args.cpu_seconds / tcal)))
     if args.cpu_queries:
         nq_s = args.cpu_queries
-    xqs = C.synth(QUERY_SEED, 0, nq_s, d, nthreads)
+    if xpool is not None:
+        nq_s = min(nq_s, xpool.shape[0])
+        xqs = np.ascontiguousarray(xpool[:nq_s])
+    else:
+        xqs = C.synth(QUERY_SEED, 0, nq_s, d, nthreads)
     t0 = time.time()
     C.knn_blas(xqs, xb, k, nthreads, lib=lib)
     t = time.time() - t0
@@ -150,10 +262,10 @@ def cpu_baseline_and_recall(args, n_total, d, k, D, I, nthreads):
     return res
 
 
-def read_pmc_traffic(cfg_name, n_local, nq):
+def read_pmc_traffic(cfg_name, n_local, nq, data="synthetic"):
     """HBM bytes per scan launch from a committed rocprofv3 --pmc summary of
-    this same workload (profiles/*_pmc_scan.json), or None."""
-    p = ROOT / "profiles" / f"pmc_scan_{cfg_name}.json"
+    this same workload (profiles/pmc_scan_<cfg>[_clustered].json), or None."""
+    p = ROOT / "profiles" / f"pmc_scan_{cfg_name}{'' if data == 'synthetic' else '_' + data}.json"
     if not p.exists():
         return None
     try:
@@ -171,6 +283,9 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="d", choices=sorted(CONFIGS))
+    ap.add_argument("--data", default="synthetic", choices=["synthetic", "clustered"],
+                    help="synthetic: counter-hash corpus/queries (exact in the storage dtype); clustered: "
+                         "unit-norm rows around one direction, fp32 queries")
     ap.add_argument("--nq", type=int, default=0, help="override query batch")
     ap.add_argument("--rows", type=int, default=0, help="override corpus rows (testing)")
     ap.add_argument("--recall-queries", type=int, default=0,
@@ -179,8 +294,27 @@ def main():
     ap.add_argument("--cpu-queries", type=int, default=0, help="fixed CPU sample (0: auto-size)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="target CPU baseline sample time")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline / recall leg")
+    ap.add_argument("--ranks-check", action="store_true", help=argparse.SUPPRESS)  # tests: report the rank, exit
     args = ap.parse_args()
 
+    plan = launch_plan(args.gpus, os.environ)
+    if plan.startswith("error"):
+        log(f"[bench] {plan}")
+        sys.exit(2)
+    if plan == "spawn":
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    if args.ranks_check:  # before any GPU work: which rank of which world this process is
+        print(json.dumps({"rank": int(os.environ.get("RANK", "0")), "world": int(os.environ.get("WORLD_SIZE", "1")),
+                          "gpus": args.gpus}), flush=True)
+        return
+
+    global torch, dist, fx
+    import torch as _torch  # before the HIP library: one runtime per process
+    import torch.distributed as _dist
+    torch, dist = _torch, _dist
+    import amd_fx  # noqa: F401
+    from rag_faiss_embedding_amd import faiss as _fx
+    fx = _fx
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -200,12 +334,10 @@ def main():
 
     t0 = time.time()
     ix = fx.IndexFlatL2(d, dtype=dtype, device=local)
-    lo, hi = build_shard(ix, rank, world, n_total, d, dtype, device)
+    lo, hi = build_shard(ix, rank, world, n_total, d, dtype, device, args.data)
     n_local = hi - lo
-    xq = torch.empty((nq, d), dtype=TORCH_DT[dtype], device=device)
-    fx.synth_fill(xq, 0, QUERY_SEED)
-    six = ShardedIndexFlatL2(d, n_total, local_index=ix,
-                             merge_fn=lambda Dg, Ig, kk: fx.merge_shards(fx.METRIC_L2, Dg, Ig, kk))
+    xq = make_queries(nq, d, dtype, device, args.data)
+    six = ShardedIndexFlatL2(d, n_total, local_index=ix)
     torch.cuda.synchronize()
     log(f"[rank {rank}] shard rows [{lo}, {hi}) built in {time.time() - t0:.1f}s")
 
@@ -226,12 +358,10 @@ def main():
     ix.profile(False)
     fallbacks = ix.last_fallbacks()
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed, scan_ms / max(launches, 1), float(fallbacks)], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        ts = torch.tensor([scan_ms / max(launches, 1)], dtype=torch.float64, device=device)
-        dist.all_reduce(ts, op=dist.ReduceOp.MAX)
-        scan_avg_ms = float(ts.item())
+        elapsed, scan_avg_ms = float(t[0].item()), float(t[1].item())
+        fallbacks = int(t[2].item())
     else:
         scan_avg_ms = scan_ms / max(launches, 1)
 
@@ -256,7 +386,7 @@ def main():
                 "frac": round(gbs / HBM_PEAK_GBS, 4)}
     # the committed PMC pass measured the default scan: no traffic figure for an opt-in variant
     variant = os.environ.get("FX_F32_SPLIT", "1") == "0"
-    roof["traffic"] = None if variant else read_pmc_traffic(args.config, n_local, nq)
+    roof["traffic"] = None if variant else read_pmc_traffic(args.config, n_local, nq, args.data)
     roof["kernel"] = "k_scan_v4" + \
         (" F32S (fp32 as 3 bf16 MFMA products)" if split else "") + " (fused MFMA distance GEMM + top-k select)"
     roof["kernel_ms_avg"] = round(scan_avg_ms, 4)
@@ -275,10 +405,14 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": SHORT_DT[dtype],
-        "data": "synthetic: counter-hash corpus/queries generated on the GPU (exact in bf16/fp16/fp32)",
+        "data": ("synthetic: counter-hash corpus/queries generated on the GPU (exact in bf16/fp16/fp32)"
+                 if args.data == "synthetic" else
+                 f"synthetic clustered: unit-norm rows base + {CLUSTER_SPREAD} N(0, I/d) generated on the GPU, "
+                 f"stored as {SHORT_DT[dtype]}; fp32 queries of the same distribution (inexact in {SHORT_DT[dtype]})"),
         "config": {
             "workload": (f"{n_total} x {d} {SHORT_DT[dtype]} flat L2 index, {nq}-query batch, top-{k}, "
-                         f"row-sharded over {world} GPU(s) + RCCL all_gather merge"),
+                         + (f"row-sharded over {world} GPUs, one RCCL all_gather + on-device merge"
+                            if world > 1 else "1 GPU")),
             "baseline_config": args.config, "corpus_rows": n_total, "dim": d, "nq": nq, "k": k,
             "rows_per_gpu": n_local, "parallelism": f"row-shard x{world}",
         },
@@ -289,7 +423,7 @@ def main():
         # the reference's call form: host float32 queries in, host D / I out
         # (PCIe both ways), same index -- reported beside `value`, never as it
         try:
-            xq_h = xq.float().cpu().numpy()
+            xq_h = xq.float().cpu().numpy()  # (fp32: exact for 16-bit synthetic queries)
             ix.search(xq_h, k)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -305,7 +439,7 @@ def main():
             log("pcie-inclusive leg failed:", e)
     if rank == 0 and not args.no_cpu:
         nthreads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
-        extra = cpu_baseline_and_recall(args, n_total, d, k, D, I, nthreads)
+        extra = cpu_baseline_and_recall(args, n_total, d, dtype, k, D, I, xq, nthreads, device)
         if world > 1:
             extra.pop("cpu_baseline", None)
         out.update(extra)

@@ -47,12 +47,17 @@ class ShardedIndexFlatL2:
             from . import faiss as fx
             local_index = fx.IndexFlatL2(d, dtype=dtype, device=device if device is not None else 0)
             local_index.set_id_offset(self.lo)
-            self._merge = lambda Dg, Ig, k: fx.merge_shards(fx.METRIC_L2, Dg, Ig, k)
-        else:
-            self._merge = merge_fn
-        if merge_fn is not None:
-            self._merge = merge_fn
+        self._merge = merge_fn if merge_fn is not None else self._device_merge
         self.local = local_index
+
+    def _device_merge(self, Dg, Ig, k):
+        """fx_merge_shards on the local index's GPU; gathered host tensors (a
+        gloo group) go there and come back."""
+        from . import faiss as fx
+        dev = torch.device("cuda", self.local.device)
+        on_host = not Dg.is_cuda
+        Dm, Im = fx.merge_shards(self.local.metric_type, Dg.to(dev), Ig.to(dev), k)
+        return (Dm.cpu(), Im.cpu()) if on_host else (Dm, Im)
 
     @property
     def ntotal(self) -> int:

@@ -1,0 +1,75 @@
+"""The row-sharded search with the REAL per-rank HIP index and the on-device
+merge (fx_merge_shards), under a world-2 process group (gloo: both ranks share
+cuda:0 on the one-GPU test box; the exchange is the same all_gather the nccl
+path runs).  Checked against the exact oracle over the whole corpus,
+including a duplicate row pair straddling the shard boundary (ties must
+break to the smaller global id).  SURVEY.md 8e; BASELINE.json metric
+"1/2/4/8 MI355X"."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, dtype, q):
+    import amd_fx  # noqa: F401
+    from oracle import cpu as C
+    from rag_faiss_embedding_amd.sharded import ShardedIndexFlatL2, shard_bounds
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(21)
+        n, d, k = 40_003, 128, 10
+        xb = rng.standard_normal((n, d)).astype(np.float32)
+        lo1, _ = shard_bounds(n, world, 1)
+        xb[lo1 - 1] = xb[lo1] = xb[7]                      # a tie across the shard boundary
+        xq = np.vstack([xb[7:8] + 0.01, rng.standard_normal((300, d)).astype(np.float32)])
+        ix = ShardedIndexFlatL2(d, n, dtype=dtype, device=0)
+        for r0 in range(0, n, 10_000):                      # every rank is handed every block
+            ix.add(xb[r0:r0 + 10_000], row0=r0)
+        assert ix.ntotal == n
+        D, I = ix.search(xq, k)
+        ref = xb if dtype == "float32" else _stored(xb, dtype)
+        Dr, Ir = C.knn_exact(xq, ref, k)
+        ids_ok = bool((I == Ir).all())
+        d_ok = bool((np.abs(D - Dr) <= 1e-5 * np.maximum(1.0, np.abs(Dr))).all())
+        q.put((rank, ids_ok, d_ok, I[0].tolist(), ix.local.last_fallbacks()))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, False, False, repr(e), -1))
+    finally:
+        dist.destroy_process_group()
+
+
+def _stored(x, dtype):
+    import torch
+    return torch.from_numpy(x).to(getattr(torch, dtype)).float().numpy()
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+def test_sharded_real_index_world2(dtype):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 2
+    procs = [ctx.Process(target=_worker, args=(r, world, port, dtype, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, ids_ok, d_ok, i0, nfb in sorted(res):
+        assert ids_ok and d_ok, (rank, i0)
+        lo1 = 40_003 // 2
+        assert i0[:3] == sorted(i0[:3]) and {7, lo1 - 1, lo1} <= set(i0[:3]), i0

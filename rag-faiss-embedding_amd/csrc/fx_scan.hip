@@ -45,9 +45,6 @@
 #ifndef FX_V4_DMAPOS
 #define FX_V4_DMAPOS 0    // MFMA pairs after which a stage's corpus pieces issue: 0 (4,6 | 4,5), 1 (1,5 | 1,5),
 #endif                    // 2 (2,6 | 2,6), 3 (3,7 | 3,7)
-#ifndef FX_V4_ATOMPUSH
-#define FX_V4_ATOMPUSH 0  // 1: push_group (branchy, one atomic per lane) instead of push_lean
-#endif
 
 namespace fx {
 
@@ -60,9 +57,7 @@ constexpr int S_NSLOT_B = 4 * 256;              // [wave][32 row norms | 32 thre
 constexpr int S_RING_OFF = S_NORM_OFF + 4 * S_NSLOT_B;
 constexpr int S_LD_OFF = S_RING_OFF + S_NS * S_STAGE;
 constexpr int S_LI_OFF = S_LD_OFF + TILE_Q * CAP * 4;
-constexpr int S_CNT_OFF = S_LI_OFF + TILE_Q * CAP * 4;
-constexpr int S_TAU_OFF = S_CNT_OFF + TILE_Q * 4;
-constexpr int S_TRASH_OFF = S_TAU_OFF + TILE_Q * 4;  // [4 waves][64 lanes] sink of the lean push
+constexpr int S_TRASH_OFF = S_LI_OFF + TILE_Q * CAP * 4;  // [4 waves][64 lanes] sink of the branch-free push
 constexpr int S_LDS_BYTES = S_TRASH_OFF + 4 * 256;
 static_assert(S_LDS_BYTES <= 160 * 1024, "LDS budget");
 
@@ -72,7 +67,8 @@ static_assert(S_LDS_BYTES <= 160 * 1024, "LDS budget");
 // results invalid; 64 per-wave s_memtime segment sums into p.stamps (results
 // valid, timing distorted by the stamps); 128 the stage's LDS-DMA pieces
 // issued as one burst after the first MFMA pair (results valid); 256 the
-// epilogue's fast path only (no pushes: results invalid)
+// epilogue's fast path only (slow tiles counted into p.stamps, no pushes:
+// results invalid)
 //
 // LN selects the shape of the corpus LDS-DMA pieces and of the LDS image:
 //   LN = 0: fragment-shaped pieces (16 rows x 64 B: each piece touches 16
@@ -109,15 +105,13 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
 
     float* lst_d = (float*)(smem + S_LD_OFF);
     int* lst_i = (int*)(smem + S_LI_OFF);
-    int* cnt = (int*)(smem + S_CNT_OFF);
-    float* tau = (float*)(smem + S_TAU_OFF);
     const int qw0 = wave * 32;  // this wave's queries (tile-local)
     const uint32_t ld_off = lds_off(lst_d), li_off = lds_off(lst_i);
     const uint32_t trash = lds_off(smem + S_TRASH_OFF) + (uint32_t)(wave * 256 + lane * 4);
-    if (lane < 32) {
-        cnt[qw0 + lane] = 0;
-        tau[qw0 + lane] = KEY_MAX;
-    }
+    // list counts and thresholds of this lane's two queries (compact_regs)
+    ListRegs lr;
+    lr.cnt[0] = lr.cnt[1] = 0;
+    lr.tau[0] = lr.tau[1] = KEY_MAX;
     unsigned* gtq = p.gtau + q0 + qw0;
     float* pubw = p.pub ? p.pub + (q0 + qw0) * p.splits * KP : nullptr;
 
@@ -194,8 +188,9 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
 #pragma unroll
     for (int n = 0; n < N; ++n) qloc[n] = qw0 + n * 16 + (lane & 15);
     const bool qv0 = q0 + qloc[0] < p.nq, qv1 = q0 + qloc[1] < p.nq;
-    // per-lane LDS addresses: tau of my two queries, my thresholds in a norm slot
-    const uint32_t tau_addr = lds_off(tau + qloc[0]);
+    // per-lane LDS addresses: my two queries' list rows, my thresholds in a norm slot
+    const uint32_t lq[N] = {ld_off + (uint32_t)(qloc[0] * CAP * 4), ld_off + (uint32_t)(qloc[1] * CAP * 4)};
+    const uint32_t li_d = li_off - ld_off;
     const uint32_t gt_lane = (uint32_t)(128 + (lane & 15) * 4);
     const uint32_t nrm_lane = (uint32_t)(rl0 * 4);
 
@@ -226,10 +221,12 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
     // ABL & 64: per-wave cycle sums {stage wait + barrier, half 0, mid-stage
     // LDS wait, half 1, epilogue, stages, slow-path tiles, slow-path cycles,
     // compaction calls, compaction cycles, group pushes, -}
-    uint64_t stq[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // [11]: slow path up to the first compaction
+    // [11]: slow path up to the first compaction; [12]: fast epilogue (tile end -> ballot decided)
+    uint64_t stq[15] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    // ABL & 1024: stamps in the slow path only ([6]-[11]) + [13] wave cycles, [14] tiles
+    if constexpr (ABL & 1024) stq[13] = __builtin_amdgcn_s_memtime();
     uint64_t s_end = 0;
     for (int t = 0; t < ntiles; ++t) {
-        float tr[N];
         unsigned gr[N];
         float gmin[N][M];  // per (query column, 16-row group) minimum key of the tile
         static_for<SPT>([&](auto JJ) {
@@ -308,9 +305,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                 });
             }
             if constexpr (LAST) {
-                // epilogue operands of this tile: the queries' thresholds
-                ds_rd32<0>(tr[0], tau_addr);
-                ds_rd32<64>(tr[1], tau_addr);
+                // epilogue operands of this tile: the queries' shared thresholds
                 const uint32_t ns = lds_base + S_NORM_OFF + (uint32_t)(t & 3) * S_NSLOT_B + wave * 256 + gt_lane;
                 ds_rd32<0>(gr[0], ns);
                 ds_rd32<64>(gr[1], ns);
@@ -400,8 +395,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
         // stage's fragments have landed
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         float tn[N];
-        tn[0] = qv0 ? fminf(tr[0], ord2f(gr[0])) : -FX_INF;
-        tn[1] = qv1 ? fminf(tr[1], ord2f(gr[1])) : -FX_INF;
+        tn[0] = qv0 ? fminf(lr.tau[0], ord2f(gr[0])) : -FX_INF;
+        tn[1] = qv1 ? fminf(lr.tau[1], ord2f(gr[1])) : -FX_INF;
         float mn[N];
 #pragma unroll
         for (int n = 0; n < N; ++n) {
@@ -411,13 +406,17 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
 #pragma unroll
             for (int m = 1; m < M; ++m) mn[n] = __builtin_fminf(mn[n], gmin[n][m]);
         }
+        if constexpr (ABL & 64) stq[12] += __builtin_amdgcn_s_memtime() - s_end;  // fast epilogue
         // unlikely: the slow path's code (pushes, compaction) is laid out
         // after the loop, so the hot path runs through without a jump over it
         // (the loop body then fits the instruction cache)
+        if constexpr (ABL & 256) {  // ablation: fast path live (slow tiles counted), no pushes
+            if (__builtin_amdgcn_ballot_w64(mn[0] <= tn[0] || mn[1] <= tn[1]) != 0) stq[6] += 1;
+        }
         if (!(ABL & (8 | 256)) && __builtin_expect(__builtin_amdgcn_ballot_w64(mn[0] <= tn[0] || mn[1] <= tn[1]) != 0, 0)) {
             // slow path: some row beats a query's threshold
             uint64_t s_sl = 0;
-            if constexpr (ABL & 64) s_sl = __builtin_amdgcn_s_memtime();
+            if constexpr (ABL & (64 | 1024)) s_sl = __builtin_amdgcn_s_memtime();
             const int trow0 = (ct0 + t) * TILE_R;
             const int rlim = p.ntotal < (int64_t)trow0 + TILE_R ? (int)p.ntotal : trow0 + TILE_R;
             {
@@ -429,48 +428,40 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                     static_for<M>([&](auto MM) {
                         constexpr int m = decltype(MM)::value;
                         if (__builtin_amdgcn_ballot_w64(gmin[n][m] <= tn[n])) {
-                            if constexpr (FX_V4_ATOMPUSH)
-                                ovf |= push_group<M, N>(acc, n, m, 15u, tn[n], qloc[n], trow0 + rl0 + m * 16, rlim,
-                                                        lst_d, lst_i, cnt, pend[n]);
-                            else
-                                ovf |= push_lean<M, N>(acc, n, m, 15u, tn[n], qloc[n], trow0 + rl0 + m * 16, rlim,
-                                                       ld_off, li_off, trash, cnt, pend[n]);
-                            if constexpr (ABL & 64) stq[10] += 1;
+                            ovf |= push_reg<M, N>(acc, n, m, 15u, tn[n], trow0 + rl0 + m * 16, rlim, lq[n], li_d, trash,
+                                                  lr.cnt[n], lane, pend[n]);
+                            if constexpr (ABL & (64 | 1024)) stq[10] += 1;
                         }
                     });
                 }
             });
-            if constexpr (ABL & 64) stq[11] += __builtin_amdgcn_s_memtime() - s_sl;
+            if constexpr (ABL & (64 | 1024)) stq[11] += __builtin_amdgcn_s_memtime() - s_sl;
             while (__builtin_amdgcn_ballot_w64(ovf)) {
                 uint64_t s_cp = 0;
-                if constexpr (ABL & 64) s_cp = __builtin_amdgcn_s_memtime();
-                compact_wave(lst_d, lst_i, cnt, tau, p.share ? gtq : nullptr, qw0, lane, pubw, p.splits, split, p.prune_rank);
-                if constexpr (ABL & 64) {
+                if constexpr (ABL & (64 | 1024)) s_cp = __builtin_amdgcn_s_memtime();
+                lr = compact_regs(lst_d, lst_i, lr, p.share ? gtq : nullptr, qw0, lane, p.pub ? pubw : nullptr, p.splits,
+                                  split, p.prune_rank);
+                if constexpr (ABL & (64 | 1024)) {
                     stq[8] += 1;
                     stq[9] += __builtin_amdgcn_s_memtime() - s_cp;
                 }
                 ovf = false;
                 static_for<N>([&](auto NN) {
                     constexpr int n = decltype(NN)::value;
-                    const float tq = (n == 0 ? qv0 : qv1) ? fminf(tau[qloc[n]], tn[n]) : -FX_INF;
+                    const float tq = (n == 0 ? qv0 : qv1) ? fminf(lr.tau[n], tn[n]) : -FX_INF;
                     const unsigned pn = pend[n];
                     pend[n] = 0u;
                     static_for<M>([&](auto MM) {
                         constexpr int m = decltype(MM)::value;
                         const unsigned el = (pn >> (4 * m)) & 15u;
-                        if (__builtin_amdgcn_ballot_w64(el != 0u)) {
-                            if constexpr (FX_V4_ATOMPUSH)
-                                ovf |= push_group<M, N>(acc, n, m, el, tq, qloc[n], trow0 + rl0 + m * 16, rlim, lst_d,
-                                                        lst_i, cnt, pend[n]);
-                            else
-                                ovf |= push_lean<M, N>(acc, n, m, el, tq, qloc[n], trow0 + rl0 + m * 16, rlim, ld_off,
-                                                       li_off, trash, cnt, pend[n]);
-                        }
+                        if (__builtin_amdgcn_ballot_w64(el != 0u))
+                            ovf |= push_reg<M, N>(acc, n, m, el, tq, trow0 + rl0 + m * 16, rlim, lq[n], li_d, trash,
+                                                  lr.cnt[n], lane, pend[n]);
                     });
                 });
             }
             }
-            if constexpr (ABL & 64) {
+            if constexpr (ABL & (64 | 1024)) {
                 stq[6] += 1;
                 stq[7] += __builtin_amdgcn_s_memtime() - s_sl;
             }
@@ -497,7 +488,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
     for (int qi = 0; qi < 32; ++qi) {
         const int q = qw0 + qi;
         if (q0 + q >= p.nq) break;
-        const int cn = min(cnt[q], CAP);
+        const int cq = qi < 16 ? __builtin_amdgcn_readlane(lr.cnt[0], qi) : __builtin_amdgcn_readlane(lr.cnt[1], qi - 16);
+        const int cn = min(cq, CAP);
         float d = lane < cn ? lst_d[q * CAP + lane] : FX_INF;
         int i = lane < cn ? lst_i[q * CAP + lane] : INT_MAX;
         sort64(d, i, lane);
@@ -507,9 +499,13 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
         }
     }
     if (p.trace && tid == 0) p.trace[blockIdx.x * 4 + 3] = wall_clock64();
-    if constexpr (ABL & 64) {
+    if constexpr (ABL & 1024) {
+        stq[13] = __builtin_amdgcn_s_memtime() - stq[13];
+        stq[14] = (uint64_t)ntiles;
+    }
+    if constexpr (ABL & (64 | 256 | 1024)) {
         if (p.stamps && lane == 0)
-            for (int i = 0; i < 12; ++i) p.stamps[((int64_t)blockIdx.x * 4 + wave) * 16 + i] = stq[i];
+            for (int i = 0; i < 15; ++i) p.stamps[((int64_t)blockIdx.x * 4 + wave) * 16 + i] = stq[i];
     }
 }
 
@@ -517,7 +513,7 @@ template <int DT, int METRIC, int KSTEPS, int ABL = 0, int LN = 1>
 static hipError_t scan_v4_t(const ScanParams& p, hipStream_t s) {
 #ifdef FX_ABLATION
     if constexpr (ABL == 0 && DT == BF16 && METRIC == L2 && KSTEPS == 24) {
-        switch (p.dbg & 511) {
+        switch (p.dbg & 2047) {
             case 1: return scan_v4_t<DT, METRIC, KSTEPS, 1, LN>(p, s);
             case 2: return scan_v4_t<DT, METRIC, KSTEPS, 2, LN>(p, s);
             case 4: return scan_v4_t<DT, METRIC, KSTEPS, 4, LN>(p, s);
@@ -532,6 +528,7 @@ static hipError_t scan_v4_t(const ScanParams& p, hipStream_t s) {
             case 128: return scan_v4_t<DT, METRIC, KSTEPS, 128, LN>(p, s);
             case 192: return scan_v4_t<DT, METRIC, KSTEPS, 192, LN>(p, s);
             case 256: return scan_v4_t<DT, METRIC, KSTEPS, 256, LN>(p, s);
+            case 1024: return scan_v4_t<DT, METRIC, KSTEPS, 1024, LN>(p, s);
             default: break;
         }
     }

@@ -72,24 +72,17 @@ __device__ __forceinline__ void ds_rd32(T& d, uint32_t addr) {
     asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(d) : "v"(addr), "i"(OFF) : "memory");
 }
 
-// A bound on the rank-th smallest key of the union of `nl` published lists
-// (float keys, `stride` apart, the first 16 entries of each read: 4 per lane
-// for up to 16 lists): the smallest v found by 8 bisection steps over the
-// ordered-uint range [lo, hi] such that at least `rank` entries are <= v (hi
-// = the caller's own rank-th key, which already qualifies).  Counting entries
-// is a valid lower bound on the rows below v (see compact_wave), so any v the
-// bisection accepts bounds the global rank-th key.
-__device__ __forceinline__ unsigned union_kth(const float* lists, int nl, int stride, unsigned hi, int rank,
-                                              int lane) {
-    unsigned kv[4];
+// A bound on the rank-th smallest key of the union of up to 16 published
+// lists (float keys, their first 16 entries: 4 per lane, as ordered uints in
+// kv, 0xFFFFFFFF where absent): the smallest v found by 8 bisection steps
+// over the ordered-uint range [lo, hi] such that at least `rank` entries are
+// <= v (hi = the caller's own rank-th key, which already qualifies).  Counting
+// entries is a valid lower bound on the rows below v (see compact_regs), so
+// any v the bisection accepts bounds the global rank-th key.
+__device__ __forceinline__ unsigned union_kth_v(const unsigned (&kv)[4], unsigned hi, int rank) {
     unsigned lo = 0xFFFFFFFFu;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int l = (lane >> 4) + 4 * i, e = lane & 15;  // list l, entry e
-        kv[i] = l < nl ? f2ord(__hip_atomic_load(lists + l * stride + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                       : 0xFFFFFFFFu;
-        lo = kv[i] < lo ? kv[i] : lo;
-    }
+    for (int i = 0; i < 4; ++i) lo = kv[i] < lo ? kv[i] : lo;
     // wave minimum: the answer lies in [lo, hi]
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -107,28 +100,111 @@ __device__ __forceinline__ unsigned union_kth(const float* lists, int nl, int st
     return hi;
 }
 
-// Compact this wave's full lists (cnt >= CAP) to their KP best; tau = KP-th,
-// published to the shared per-query threshold.  Lists are owned by one wave.
-// The 32 counts are read in one LDS access (lane i: query qw0 + i) and only
-// the full lists are visited.
+// LDS store through an explicit byte offset (the lean push below picks the
+// offset per lane instead of branching)
+__device__ __forceinline__ void ds_wr32(uint32_t off, float v) {
+    asm volatile("ds_write_b32 %0, %1" ::"v"(off), "v"(v) : "memory");
+}
+__device__ __forceinline__ void ds_wr32(uint32_t off, int v) {
+    asm volatile("ds_write_b32 %0, %1" ::"v"(off), "v"(v) : "memory");
+}
+
+// Per-wave candidate lists of k_scan_v4.  The wave owns 32 queries: query
+// column c of accumulator half n (lanes with lane & 15 == c, n = 0, 1) is
+// tile-local query qw0 + 16 n + c.  Each list lives in LDS ([query][CAP] keys
+// and rows); its entry count and its pruning threshold live in registers
+// (cntv[n], tauv[n]), the same value in the 4 lanes that hold the query, so a
+// push reserves its slots without an LDS atomic round trip.
+
+// x of lane ^ 16 / lane ^ 32 without the LDS crossbar: gfx950's
+// v_permlane16_swap (odd 16-lane rows of the first operand <-> even rows of
+// the second) and v_permlane32_swap (upper half of the first <-> lower half of
+// the second) on two copies of x.  The s_nop covers a VALU write of the
+// copies just before (inline asm is not padded by the compiler).
+__device__ __forceinline__ int lane_xor16(int x, int lane) {
+    int a = x, b = x;
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+    return (lane & 16) ? a : b;
+}
+__device__ __forceinline__ int lane_xor32(int x, int lane) {
+    int a = x, b = x;
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+    return (lane & 32) ? a : b;
+}
+
+// Exclusive prefix and total of `c` over the 4 lanes that hold one query
+// (lane >> 4 = 0..3, the same lane & 15).
+__device__ __forceinline__ void quad_prefix(int c, int lane, int& excl, int& total) {
+    const int a = lane_xor16(c, lane);
+    const int s2 = c + a;
+    const int b = lane_xor32(s2, lane);
+    excl = ((lane & 16) ? a : 0) + ((lane & 32) ? b : 0);
+    total = s2 + b;
+}
+
+// Push the entries of accumulator group (m, n) selected by `elig` (4 bits)
+// that pass `tn` into the lane's query list; entries that find the list full
+// are recorded in `pend` (bit 4m+i) for a retry after compaction (returns
+// whether any were).  Branch-free: every lane stores all 4 of its entries,
+// those that do not pass (or find the list full) into the wave's trash word.
+// lq: LDS byte offset of the query's key row; li_d: rows array - keys array.
+template <int M, int N>
+__device__ __forceinline__ bool push_reg(const f32x4 (&acc)[M][N], int n, int m, unsigned elig, float tn, int row0,
+                                         int rlim, uint32_t lq, uint32_t li_d, uint32_t trash, int& cntv, int lane,
+                                         unsigned& pend) {
+    unsigned msk = 0u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) msk |= (acc[m][n][i] <= tn && row0 + i < rlim) ? (1u << i) : 0u;
+    msk &= elig;
+    int excl, total;
+    quad_prefix((int)__popc(msk), lane, excl, total);
+    const int s = cntv + excl;
+    unsigned late = 0u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int slot = s + (int)__popc(msk & ((1u << i) - 1u));
+        const bool take = (msk >> i) & 1u;
+        const bool ok = take && slot < CAP;
+        const uint32_t e = lq + (uint32_t)slot * 4u;
+        ds_wr32(ok ? e : trash, acc[m][n][i]);
+        ds_wr32(ok ? e + li_d : trash, row0 + i);
+        late |= (take && !ok) ? (1u << i) : 0u;
+    }
+    cntv += total;
+    pend |= late << (4 * m);
+    return late != 0u;
+}
+
+// Compact this wave's full lists (cntv >= CAP) to their KP best; the list's
+// threshold becomes its rank-th key (rank = KP unless the union bound is on),
+// published to the shared per-query threshold.  Only the full lists are
+// visited.
 //
-// pub (k_scan_v4, k <= KP): the compacted list is also published to
-// pub[query][split][KP], and the shared threshold becomes the KP-th smallest
-// key of the union of the published lists of up to 16 splits (this one's
-// window of 16) -- a valid bound on the query's global KP-th key, because
-// every published entry is the key of a distinct row of its split (a list
-// read while its split rewrites it mixes two versions of the same
-// improving list: entry i of either version still has i + 1 rows of that
-// split at or below it, so counting entries never over-counts rows).  A
-// split that starts late then prunes with what all earlier splits found,
-// not only with the best single split's KP-th key.  rank (<= 16, >= k): the
-// union bound is taken at this rank, below KP -- every dropped row then lies
-// above the final shared threshold, which k_refine folds into its
-// certification bound (RefineParams.gtau).
-__device__ __noinline__ void compact_wave(float* lst_d, int* lst_i, int* cnt, float* tau, unsigned* gtq, int qw0,
-                                          int lane, float* pub = nullptr, int splits = 0, int split = 0,
-                                          int rank = KP) {
-    uint64_t full = __builtin_amdgcn_ballot_w64(lane < 32 && cnt[qw0 + (lane & 31)] >= CAP);
+// pub (k <= KP): the compacted list is also published to pub[query][split][KP],
+// and the shared threshold becomes the rank-th smallest key of the union of
+// the published lists of up to 16 splits (this one's window of 16) -- a valid
+// bound on the query's global rank-th key, because every published entry is
+// the key of a distinct row of its split (a list read while its split
+// rewrites it mixes two versions of the same improving list: entry i of
+// either version still has i + 1 rows of that split at or below it, so
+// counting entries never over-counts rows).  A split that starts late then
+// prunes with what all earlier splits found.  rank (>= k): every dropped row
+// lies above the final shared threshold, which k_refine folds into its
+// certification bound (RefineParams.gtau).  The union reads of the full
+// lists are issued together (one memory round trip per 4 lists, not one per
+// list).
+struct ListRegs {
+    int cnt[2];
+    float tau[2];
+};
+__device__ __noinline__ ListRegs compact_regs(float* lst_d, int* lst_i, ListRegs r, unsigned* gtq, int qw0, int lane,
+                                              float* pub, int splits, int split, int rank) {
+    int (&cntv)[2] = r.cnt;
+    float (&tauv)[2] = r.tau;
+    const uint64_t f0 = __builtin_amdgcn_ballot_w64(lane < 16 && cntv[0] >= CAP);
+    const uint64_t f1 = __builtin_amdgcn_ballot_w64(lane < 16 && cntv[1] >= CAP);
+    const uint64_t all = (f0 & 0xffffull) | ((f1 & 0xffffull) << 16);
+    uint64_t full = all;
     while (full) {
         const int qi = __builtin_ctzll(full);
         full &= full - 1;
@@ -140,97 +216,52 @@ __device__ __noinline__ void compact_wave(float* lst_d, int* lst_i, int* cnt, fl
             lst_d[q * CAP + lane] = d;
             lst_i[q * CAP + lane] = i;
         }
-        // the list keeps KP entries; the threshold is its rank-th key (rank
-        // = KP unless the union bound is on): published to gtau too, so the
-        // final gtau stays below every split's local threshold (k_refine)
-        if (lane == rank - 1) {
-            tau[q] = d;
-            if (gtq) atomicMin(gtq + qi, f2ord(d));  // null: no cross-split pruning (k > KP)
+        const float dr = __shfl(d, rank - 1, 64);
+        if ((lane & 15) == (qi & 15)) {
+            if (qi < 16) { tauv[0] = dr; cntv[0] = KP; }
+            else { tauv[1] = dr; cntv[1] = KP; }
         }
-        if (lane == 0) cnt[q] = KP;
-        if (pub && gtq) {
-            float* qp = pub + (int64_t)qi * splits * KP;  // pub: this wave's first query
-            if (lane < KP) __hip_atomic_store(qp + split * KP + lane, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const int w0 = split & ~15;
-            const int nsp = splits - w0 < 16 ? splits - w0 : 16;
-            const unsigned own = f2ord(__shfl(d, rank - 1, 64));
-            const unsigned v = union_kth(qp + w0 * KP, nsp, KP, own, rank, lane);
+        // published to gtau too, so the final gtau stays below every split's
+        // local threshold (k_refine); null gtq: no cross-split pruning (k > KP)
+        if (gtq && lane == 0) atomicMin(gtq + qi, f2ord(dr));
+        if (pub && gtq && lane < KP)
+            __hip_atomic_store(pub + ((int64_t)qi * splits + split) * KP + lane, d, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (!(pub && gtq)) return r;
+    // union bounds, up to 4 lists per memory round trip
+    const int w0 = split & ~15;
+    const int nsp = splits - w0 < 16 ? splits - w0 : 16;
+    uint64_t rest = all;
+    while (rest) {
+        int qs[4];
+        unsigned kv[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            qs[u] = rest ? __builtin_ctzll(rest) : -1;
+            if (rest) rest &= rest - 1;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const float* lists = pub + ((int64_t)(qs[u] < 0 ? 0 : qs[u]) * splits + w0) * KP;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int l = (lane >> 4) + 4 * j, e = lane & 15;  // list l, entry e
+                kv[u][j] = (qs[u] >= 0 && l < nsp)
+                               ? f2ord(__hip_atomic_load(lists + l * KP + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                               : 0xFFFFFFFFu;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (qs[u] < 0) break;
+            const int qi = qs[u];
+            const unsigned own = f2ord(__shfl(qi < 16 ? tauv[0] : tauv[1], qi & 15, 64));
+            const unsigned v = union_kth_v(kv[u], own, rank);
             if (lane == 0 && v < own) atomicMin(gtq + qi, v);
         }
     }
-}
-
-// push the entries of accumulator group (m, n) selected by `elig` (4 bits)
-// that pass `tn` into query q's list; entries that find the list full are
-// recorded in `pend` (bit 4m+i) for a retry after compaction.  One LDS atomic
-// per lane reserves all of its slots (the list belongs to this wave; the
-// atomic only orders the four lanes that hold query q), so a push costs one
-// LDS round trip however many of the lane's 4 rows pass.
-template <int M, int N, int CAPL = CAP>
-__device__ __forceinline__ bool push_group(const f32x4 (&acc)[M][N], int n, int m, unsigned elig, float tn, int q,
-                                           int row0, int rlim, float* lst_d, int* lst_i, int* cnt, unsigned& pend) {
-    unsigned msk = 0u;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-        if (((elig >> i) & 1u) && acc[m][n][i] <= tn && row0 + i < rlim) msk |= 1u << i;
-    bool ovf = false;
-    if (msk) {
-        int s = atomicAdd(&cnt[q], __popc(msk));
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            if ((msk >> i) & 1u) {
-                if (s < CAPL) {
-                    lst_d[q * CAPL + s] = acc[m][n][i];
-                    lst_i[q * CAPL + s] = row0 + i;
-                } else {
-                    pend |= 1u << (m * 4 + i);
-                    ovf = true;
-                }
-                ++s;
-            }
-        }
-    }
-    return ovf;
-}
-
-// LDS store through an explicit byte offset (the lean push below picks the
-// offset per lane instead of branching)
-__device__ __forceinline__ void ds_wr32(uint32_t off, float v) {
-    asm volatile("ds_write_b32 %0, %1" ::"v"(off), "v"(v) : "memory");
-}
-__device__ __forceinline__ void ds_wr32(uint32_t off, int v) {
-    asm volatile("ds_write_b32 %0, %1" ::"v"(off), "v"(v) : "memory");
-}
-
-// push_group without divergent branches (k_scan_v4's slow path): every lane
-// takes one LDS atomic on cnt[q] (adding 0 when none of its 4 rows passes)
-// and stores all 4 of its entries -- entries that do not pass, or find the
-// list full, go to the wave's trash word `trash` instead of a list slot.  The
-// group costs a fixed ~50 instructions and one LDS round trip, however the
-// passing rows are spread over the lanes.  ld / li: LDS byte offsets of the
-// key and row arrays ([query][CAP]).
-template <int M, int N>
-__device__ __forceinline__ bool push_lean(const f32x4 (&acc)[M][N], int n, int m, unsigned elig, float tn, int q,
-                                          int row0, int rlim, uint32_t ld, uint32_t li, uint32_t trash, int* cnt,
-                                          unsigned& pend) {
-    unsigned msk = 0u;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) msk |= (acc[m][n][i] <= tn && row0 + i < rlim) ? (1u << i) : 0u;
-    msk &= elig;
-    const int s = atomicAdd(&cnt[q], (int)__popc(msk));
-    unsigned late = 0u;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int slot = s + (int)__popc(msk & ((1u << i) - 1u));
-        const bool take = (msk >> i) & 1u;
-        const bool ok = take && slot < CAP;
-        const uint32_t e = (uint32_t)(q * CAP + slot) * 4u;
-        ds_wr32(ok ? ld + e : trash, acc[m][n][i]);
-        ds_wr32(ok ? li + e : trash, row0 + i);
-        late |= (take && !ok) ? (1u << i) : 0u;
-    }
-    pend |= late << (4 * m);
-    return late != 0u;
+    return r;
 }
 
 // minimum of the 4 keys of an accumulator group: two VALU ops (fminf would

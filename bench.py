@@ -54,8 +54,8 @@ CONFIGS = {
 }
 # exact-oracle recall sample per config (>= 1000 queries where the
 # oracle allows; the full-corpus streaming oracle costs ~0.25 s per query on (d)
-# and ~1.2 s on (e) with 16 host cores)
-RECALL_QUERIES = {"d": 256, "b": 1000, "e": 32}
+# and ~1.3 s on (e) with 16 host cores: the (e) leg takes ~5 min)
+RECALL_QUERIES = {"d": 256, "b": 1000, "e": 256}
 SHORT_DT = {"float32": "f32", "bfloat16": "bf16", "float16": "f16"}
 # MI355X_MICROARCH.md: dense MFMA peaks (TFLOP/s) and HBM3E peak (GB/s)
 MFMA_PEAK = {"float32": 157.3, "bfloat16": 2500.0, "float16": 2500.0}
@@ -357,6 +357,10 @@ def main():
     scan_ms, merge_ms, launches = ix.profile_read()
     ix.profile(False)
     fallbacks = ix.last_fallbacks()
+    try:
+        exact_fb = ix.last_exact_fallbacks()
+    except AttributeError:  # an older library under FX_INDEX_LIB (same-box A/B)
+        exact_fb = None
     if world > 1:
         t = torch.tensor([elapsed, scan_ms / max(launches, 1), float(fallbacks)], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -417,6 +421,7 @@ def main():
             "rows_per_gpu": n_local, "parallelism": f"row-shard x{world}",
         },
         "fallback_queries_last_step": fallbacks,
+        "exact_fallback_queries_last_step": exact_fb,
         "roofline": roof,
     }
     if world == 1:

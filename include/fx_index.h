@@ -122,9 +122,12 @@ int fx_index_search(FxIndex* index, int64_t nq, const void* q, int q_dtype, int 
                     int k, float* D, int64_t* I, int out_mem);
 
 /* Number of queries of the last search whose top-k could not be certified
- * from the candidate margin and were re-ranked by the exact scan fallback
- * (after an FX_MEM_DEVICE search this synchronises the index stream). */
+ * from the scan's candidate margin and were re-scanned with a wide candidate
+ * set (after an FX_MEM_DEVICE search this synchronises the index stream). */
 int fx_index_last_fallbacks(FxIndex* index, int64_t* out);
+/* Of those, the queries the re-scan could not certify either, re-ranked by
+ * the exact fp64 scan of every row. */
+int fx_index_last_exact_fallbacks(FxIndex* index, int64_t* out);
 
 /* IndexFlatL2 reset (faiss_store.py:124-128). Keeps the HBM allocation. */
 int fx_index_reset(FxIndex* index);

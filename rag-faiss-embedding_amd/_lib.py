@@ -57,6 +57,7 @@ SIGNATURES = {
     "fx_index_add": (_i, [_vp, _i64, _vp, _i, _i]),
     "fx_index_search": (_i, [_vp, _i64, _vp, _i, _i, _i, _vp, _vp, _i]),
     "fx_index_last_fallbacks": (_i, [_vp, ctypes.POINTER(_i64)]),
+    "fx_index_last_exact_fallbacks": (_i, [_vp, ctypes.POINTER(_i64)]),
     "fx_index_reset": (_i, [_vp]),
     "fx_index_reconstruct_n": (_i, [_vp, _i64, _i64, _vp]),
     "fx_index_write": (_i, [_vp, ctypes.c_char_p]),
@@ -68,8 +69,17 @@ SIGNATURES = {
                                    ctypes.POINTER(_i64)]),
 }
 
+# FX_INDEX_LIB selects another build (same-box A/B of an older library): a
+# symbol that build predates is left unbound instead of failing the import;
+# the in-tree library must export every symbol
+_AB_BUILD = "FX_INDEX_LIB" in os.environ
 for _name, (_res, _args) in SIGNATURES.items():
-    _fn = getattr(lib, _name)
+    try:
+        _fn = getattr(lib, _name)
+    except AttributeError:
+        if not _AB_BUILD:
+            raise
+        continue
     _fn.restype = _res
     _fn.argtypes = _args
 

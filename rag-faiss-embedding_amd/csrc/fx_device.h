@@ -7,6 +7,8 @@
 #include <float.h>
 #include <limits.h>
 
+#include <utility>
+
 namespace fx {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -61,29 +63,87 @@ __device__ __forceinline__ bool key_lt(float d1, Id i1, float d2, Id i2) {
     return d1 < d2 || (d1 == d2 && i1 < i2);
 }
 
-template <typename Id>
-__device__ __forceinline__ void cmpx(float& d, Id& i, int lane, int stride, bool asc) {
-    float od = __shfl_xor(d, stride, 64);
-    Id oi = __shfl_xor(i, stride, 64);
-    bool lower = (lane & stride) == 0;
-    bool take = (lower == asc) ? key_lt(od, oi, d, i) : key_lt(d, i, od, oi);
+template <int... Is, typename F>
+__device__ __forceinline__ void static_for_impl(std::integer_sequence<int, Is...>, F&& f) {
+    (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    static_for_impl(std::make_integer_sequence<int, N>{}, f);
+}
+
+// x of lane ^ 16 / lane ^ 32 without the LDS crossbar: gfx950's
+// v_permlane16_swap (odd 16-lane rows of the first operand <-> even rows of
+// the second) and v_permlane32_swap (upper half of the first <-> lower half of
+// the second) on two copies of x.  The s_nop covers a VALU write of the
+// copies just before (inline asm is not padded by the compiler).
+__device__ __forceinline__ int lane_xor16(int x, int lane) {
+    int a = x, b = x;
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+    return (lane & 16) ? a : b;
+}
+__device__ __forceinline__ int lane_xor32(int x, int lane) {
+    int a = x, b = x;
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+    return (lane & 32) ? a : b;
+}
+// x of lane ^ S for S = 1 .. 32, all on the VALU: DPP inside 16-lane rows
+// (quad_perm for 1 and 2; row_ror for 4 and 8: ror:N reads lane - N mod 16),
+// the permlane swaps across rows
+template <int S>
+__device__ __forceinline__ int lane_xor(int x, int lane) {
+    if constexpr (S == 1) return __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    else if constexpr (S == 2) return __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false);  // [2,3,0,1]
+    else if constexpr (S == 4) {
+        const int a = __builtin_amdgcn_update_dpp(0, x, 0x124, 0xF, 0xF, false);  // row_ror:4: lane - 4
+        const int b = __builtin_amdgcn_update_dpp(0, x, 0x12C, 0xF, 0xF, false);  // row_ror:12: lane + 4
+        return (lane & 4) ? a : b;
+    } else if constexpr (S == 8) return __builtin_amdgcn_update_dpp(0, x, 0x128, 0xF, 0xF, false);  // row_ror:8
+    else if constexpr (S == 16) return lane_xor16(x, lane);
+    else return lane_xor32(x, lane);
+}
+template <int S>
+__device__ __forceinline__ float lane_xor(float x, int lane) {
+    return __int_as_float(lane_xor<S>(__float_as_int(x), lane));
+}
+template <int S>
+__device__ __forceinline__ long long lane_xor(long long x, int lane) {
+    const int lo = lane_xor<S>((int)(x & 0xffffffffll), lane), hi = lane_xor<S>((int)(x >> 32), lane);
+    return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
+// ---------------------------------------------------------------------------
+// wave-level (64-lane) bitonic helpers on (key, id) pairs, ascending,
+// ties -> smaller id.  Used for LDS list compaction and every merge.  The
+// partner exchange runs on the VALU (lane_xor), branch-free compares.
+// ---------------------------------------------------------------------------
+template <int S, typename Id>
+__device__ __forceinline__ void cmpx_s(float& d, Id& i, int lane, bool asc) {
+    const float od = lane_xor<S>(d, lane);
+    const Id oi = lane_xor<S>(i, lane);
+    const bool lower = (lane & S) == 0;
+    const bool o_lt = (od < d) | ((od == d) & (oi < i));
+    const bool m_lt = (d < od) | ((d == od) & (i < oi));
+    const bool take = (lower == asc) ? o_lt : m_lt;
     d = take ? od : d;
     i = take ? oi : i;
 }
 
 template <typename Id>
 __device__ __forceinline__ void sort64(float& d, Id& i, int lane) {
-#pragma unroll
-    for (int size = 2; size <= 64; size <<= 1) {
-#pragma unroll
-        for (int stride = size >> 1; stride > 0; stride >>= 1) cmpx(d, i, lane, stride, (lane & size) == 0);
-    }
+    static_for<6>([&](auto L) {  // size = 2 << L
+        constexpr int size = 2 << decltype(L)::value;
+        const bool asc = (lane & size) == 0;
+        static_for<decltype(L)::value + 1>([&](auto T) {  // stride = size / 2 >> T
+            constexpr int stride = (size >> 1) >> decltype(T)::value;
+            cmpx_s<stride>(d, i, lane, asc);
+        });
+    });
 }
 
 template <typename Id>
 __device__ __forceinline__ void merge64(float& d, Id& i, int lane) {  // bitonic -> ascending
-#pragma unroll
-    for (int stride = 32; stride > 0; stride >>= 1) cmpx(d, i, lane, stride, true);
+    static_for<6>([&](auto T) { cmpx_s<(32 >> decltype(T)::value)>(d, i, lane, true); });
 }
 
 // best (ascending, one per lane) <- the 64 smallest of best U cand (cand sorted ascending)

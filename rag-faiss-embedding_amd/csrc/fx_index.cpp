@@ -155,6 +155,9 @@ struct FxIndex {
     // search workspace
     DevBuf qin, qf32, qop, qeps, qrho, cand_d, cand_i, cand2_d, cand2_i, dws, iws, flag, fbc_d, fbc_i, stage, gtau,
         trace, dbgbuf, stamps, pub;
+    // the re-scan of uncertified queries (plan_rescan): its own query
+    // operands, thresholds, candidate lists and flagged list
+    DevBuf rq_f32, rq_op, rq_eps, rq_rho, rq_shift, rq_gtau, rq_cand_d, rq_cand_i, rq_flag;
     // scan image (ImageKind; rows [0, img_rows) current).  L2 images are
     // centred (Options.centre): mu = mean of a row sample, recomputed (and the
     // image rebuilt) whenever ntotal has doubled since (mu_rows), so the
@@ -181,8 +184,9 @@ struct FxIndex {
     int64_t last_fallbacks = 0;
     // uncertified count of the last search, copied stream-ordered into pinned
     // memory; read (after a stream sync) only when asked for (fb_pending)
-    int* pin_nf = nullptr;
+    int* pin_nf = nullptr;  // [0] queries re-scanned, [1] queries sent to the exact scan
     bool fb_pending = false;
+    int64_t last_exact = 0;
     // profiling
     bool profile = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_scan, ev_merge;
@@ -306,8 +310,8 @@ bool use_reduce(const FxIndex* h, int k, int64_t nq, int splits) {
 
 hipError_t ensure_pinned_count(FxIndex* h) {
     if (h->pin_nf) return hipSuccess;
-    hipError_t e = hipHostMalloc((void**)&h->pin_nf, sizeof(int), hipHostMallocDefault);
-    if (e == hipSuccess) *h->pin_nf = 0;
+    hipError_t e = hipHostMalloc((void**)&h->pin_nf, 2 * sizeof(int), hipHostMallocDefault);
+    if (e == hipSuccess) h->pin_nf[0] = h->pin_nf[1] = 0;
     return e;
 }
 
@@ -381,7 +385,80 @@ struct SearchPlan {
     PrepParams pp{};
     bool reduce = false;
     size_t ncand = 0;
+    // the re-scan of the queries pass 1 left uncertified (plan_rescan)
+    ScanParams sp2{};
+    RefineParams rp2{};
+    PrepParams pp2{};
+    int* n_exact = nullptr;  // queries the re-scan left uncertified too (-> exact scan)
 };
+
+// The re-scan of the queries pass 1 could not certify (rows flag_list[0 ..
+// n_flag) of the batch, gathered on the device): the same MFMA scan over
+// them without cross-split pruning and with ~k1/4 corpus splits, then
+// k_refine_big re-ranking k1 = max(512, 4k) approx candidates exactly, so the
+// certification bound sits near the k1-th key instead of the ~2k-th.  Its
+// uncertified queries go to the exact scan.  Launched always; every kernel
+// reads the flagged count and exits at once when it is 0.
+hipError_t plan_rescan(FxIndex* h, SearchPlan& P) {
+    hipError_t e;
+    const int64_t nq = P.nq;
+    const int k1 = std::min(2 * FX_BIG_K, std::max(512, 4 * P.k));
+    int* n_flag = P.rp.n_flag;
+    if ((e = h->rq_f32.ensure((size_t)P.nq_pad * h->kdim * 4)) != hipSuccess) return e;
+    if ((e = h->rq_op.ensure((size_t)P.nq_pad * h->row_bytes)) != hipSuccess) return e;
+    if ((e = h->rq_eps.ensure((size_t)nq * 4)) != hipSuccess) return e;
+    if ((e = h->rq_rho.ensure((size_t)nq * 4)) != hipSuccess) return e;
+    if ((e = h->rq_shift.ensure((size_t)nq * 8)) != hipSuccess) return e;
+    if ((e = h->rq_gtau.ensure((size_t)P.nq_pad * 4)) != hipSuccess) return e;
+    if ((e = h->rq_flag.ensure((size_t)(nq + 1) * 4)) != hipSuccess) return e;
+    PrepParams& pp = P.pp2;
+    pp = P.pp;
+    pp.q = h->qf32.p;  // pass 1's fp32 copy of the batch, rows padded to kdim
+    pp.q_dt = F32;
+    pp.d = h->kdim;
+    pp.qidx = P.rp.flag_list;
+    pp.nq_dev = n_flag;
+    pp.qf32 = (float*)h->rq_f32.p;
+    pp.qop = h->rq_op.p;
+    pp.qeps = (float*)h->rq_eps.p;
+    pp.qrho = (float*)h->rq_rho.p;
+    pp.qshift = (double*)h->rq_shift.p;
+    ScanParams& sp = P.sp2;
+    sp = P.sp;
+    plan_scan(h, nq, k1, sp);  // k1 > KP: share = 0, >= k1/4 splits
+    sp.qop = (const char*)h->rq_op.p;
+    sp.gtau = (unsigned*)h->rq_gtau.p;
+    sp.pub = nullptr;
+    sp.prune_rank = KP;
+    sp.dbg = 0;
+    sp.trace = nullptr;
+    sp.dbgbuf = nullptr;
+    sp.stamps = nullptr;
+    sp.nq_dev = n_flag;
+    const size_t ncand = (size_t)sp.n_qtiles * sp.splits * TILE_Q * KP;
+    if ((e = h->rq_cand_d.ensure(ncand * 4)) != hipSuccess) return e;
+    if ((e = h->rq_cand_i.ensure(ncand * 4)) != hipSuccess) return e;
+    sp.cand_d = (float*)h->rq_cand_d.p;
+    sp.cand_i = (int*)h->rq_cand_i.p;
+    RefineParams& rp = P.rp2;
+    rp = P.rp;
+    rp.cand_d = sp.cand_d;
+    rp.cand_i = sp.cand_i;
+    rp.splits = sp.splits;
+    rp.qf32 = pp.qf32;
+    rp.qeps = pp.qeps;
+    rp.qrho = pp.qrho;
+    rp.qshift = pp.qshift;
+    rp.k1 = k1;
+    rp.gtau = nullptr;
+    rp.nq_dev = n_flag;
+    rp.out_idx = P.rp.flag_list;
+    P.n_exact = (int*)h->rq_flag.p;
+    rp.n_flag = P.n_exact;
+    rp.flag_list = P.n_exact + 1;
+    rp.force_fb = h->opt.force_fallback == 2;
+    return hipSuccess;
+}
 
 hipError_t plan_search(FxIndex* h, int64_t nq, const void* qdev, int q_dtype, int k, float* Dd, int64_t* Id,
                        SearchPlan& P) {
@@ -415,6 +492,8 @@ hipError_t plan_search(FxIndex* h, int64_t nq, const void* qdev, int q_dtype, in
     pp.mbits = h->max_sq_bits;
     pp.img_bits = img ? h->max_sq_bits + 1 : h->max_sq_bits;
     pp.mu = img && h->centred ? (const float*)h->centre.p : nullptr;
+    pp.qidx = nullptr;
+    pp.nq_dev = nullptr;
 
     ScanParams& sp = P.sp;
     plan_scan(h, nq, k, sp);
@@ -446,6 +525,7 @@ hipError_t plan_search(FxIndex* h, int64_t nq, const void* qdev, int q_dtype, in
     sp.trace = nullptr;
     sp.dbgbuf = nullptr;
     sp.stamps = nullptr;
+    sp.nq_dev = nullptr;
 
     if ((e = h->flag.ensure((size_t)(nq + 1) * 4)) != hipSuccess) return e;
     RefineParams& rp = P.rp;
@@ -470,8 +550,10 @@ hipError_t plan_search(FxIndex* h, int64_t nq, const void* qdev, int q_dtype, in
     // at nq = 1); issue 4 chunks of loads at a time (nq = 1: 0.84 -> ~0.3 ms)
     rp.prefetch = nq <= 256 ? 4 : 1;
     rp.k1 = big_k1(k);
-    rp.force_fb = h->opt.force_fallback;
+    rp.force_fb = h->opt.force_fallback != 0;
     rp.gtau = sp.share ? sp.gtau : nullptr;
+    rp.nq_dev = nullptr;
+    rp.out_idx = nullptr;
     P.reduce = use_reduce(h, k, nq, sp.splits);
     if (P.reduce) {
         const size_t nred = (size_t)sp.n_qtiles * ((sp.splits + 15) / 16) * TILE_Q * KP;
@@ -481,7 +563,7 @@ hipError_t plan_search(FxIndex* h, int64_t nq, const void* qdev, int q_dtype, in
     const size_t nfb = (size_t)std::max<int64_t>(4096, nq) * k;
     if ((e = h->fbc_d.ensure(nfb * 4)) != hipSuccess) return e;
     if ((e = h->fbc_i.ensure(nfb * 4)) != hipSuccess) return e;
-    return hipSuccess;
+    return plan_rescan(h, P);
 }
 
 // Enqueue the planned search on s: query preparation, scan, candidate
@@ -513,15 +595,21 @@ hipError_t enqueue_search(FxIndex* h, SearchPlan& P, hipStream_t s, bool timed, 
     if ((e = launch_refine(h->dtype, h->metric, rp, s)) != hipSuccess) return e;
     if (timed && (e = hipEventRecord(ev[2], s)) != hipSuccess) return e;
     // Certification result: uncertified queries (rare: only when the
-    // candidate margin is inside the scan's rounding bound) are re-ranked by
-    // the exact scan.  Decided on the device: the fallback kernels are always
-    // enqueued and exit at once when the refine flagged nothing, so no host
-    // round trip sits inside the search.
-    if (P.sp.dbg == 0)
-        e = launch_exact_fallback(h->dtype, h->metric, h->codes, h->row_bytes, h->kdim, h->ntotal, P.rp.qf32,
-                                  P.rp.n_flag, P.k, h->id_offset, (float*)h->fbc_d.p, (int*)h->fbc_i.p, P.rp.D,
-                                  P.rp.I, s);
-    return e;
+    // candidate margin is inside the scan's rounding bound) are re-scanned
+    // with a wide candidate set (plan_rescan), and what that still cannot
+    // certify is re-ranked by the exact scan.  Decided on the device: these
+    // kernels are always enqueued and exit at once when nothing was flagged,
+    // so no host round trip sits inside the search.
+    if (P.sp.dbg != 0) return hipSuccess;
+    if ((e = launch_prep_queries(P.pp2, s)) != hipSuccess) return e;
+    if ((e = hipMemsetD32Async((hipDeviceptr_t)P.sp2.gtau, 0xff800000u, (size_t)P.nq_pad, s)) != hipSuccess)
+        return e;
+    if ((e = launch_scan(P.scan_dt, h->metric, P.sp2, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(P.n_exact, 0, 4, s)) != hipSuccess) return e;
+    if ((e = launch_refine(h->dtype, h->metric, P.rp2, s)) != hipSuccess) return e;
+    return launch_exact_fallback(h->dtype, h->metric, h->codes, h->row_bytes, h->kdim, h->ntotal, P.rp.qf32,
+                                 P.n_exact, P.k, h->id_offset, (float*)h->fbc_d.p, (int*)h->fbc_i.p, P.rp.D, P.rp.I,
+                                 s);
 }
 
 template <typename T>
@@ -587,6 +675,8 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
     }
     HIP_TRY(ensure_pinned_count(h));
     HIP_TRY(hipMemcpyAsync(h->pin_nf, P.rp.n_flag, 4, hipMemcpyDeviceToHost, s));
+    if (P.sp.dbg == 0) HIP_TRY(hipMemcpyAsync(h->pin_nf + 1, P.n_exact, 4, hipMemcpyDeviceToHost, s));
+    else h->pin_nf[1] = 0;
     h->fb_pending = true;
     if (!h->opt.cand.empty()) {
         HIP_TRY(hipStreamSynchronize(s));
@@ -613,7 +703,8 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
         HIP_TRY(hipMemcpyAsync(D, Dd, (size_t)nq * k * 4, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipMemcpyAsync(I, Id, (size_t)nq * k * 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
-        h->last_fallbacks = *h->pin_nf;
+        h->last_fallbacks = h->pin_nf[0];
+        h->last_exact = h->pin_nf[1];
         h->fb_pending = false;
     }
     return FX_OK;
@@ -634,7 +725,11 @@ std::vector<uint64_t> graph_key(const FxIndex* h, int64_t nq, int q_dtype, int k
             (uint64_t)(uintptr_t)h->pub.p, (uint64_t)(uintptr_t)h->cand_d.p, (uint64_t)(uintptr_t)h->cand_i.p,
             (uint64_t)(uintptr_t)h->cand2_d.p, (uint64_t)(uintptr_t)h->cand2_i.p,
             (uint64_t)(uintptr_t)h->dws.p, (uint64_t)(uintptr_t)h->iws.p,
-            (uint64_t)(uintptr_t)h->flag.p, (uint64_t)(uintptr_t)h->fbc_d.p, (uint64_t)(uintptr_t)h->fbc_i.p};
+            (uint64_t)(uintptr_t)h->flag.p, (uint64_t)(uintptr_t)h->fbc_d.p, (uint64_t)(uintptr_t)h->fbc_i.p,
+            (uint64_t)(uintptr_t)h->rq_f32.p, (uint64_t)(uintptr_t)h->rq_op.p, (uint64_t)(uintptr_t)h->rq_eps.p,
+            (uint64_t)(uintptr_t)h->rq_rho.p, (uint64_t)(uintptr_t)h->rq_shift.p, (uint64_t)(uintptr_t)h->rq_gtau.p,
+            (uint64_t)(uintptr_t)h->rq_cand_d.p, (uint64_t)(uintptr_t)h->rq_cand_i.p,
+            (uint64_t)(uintptr_t)h->rq_flag.p};
 }
 
 void graph_release(FxIndex* h) {
@@ -669,7 +764,7 @@ hipError_t graph_build(FxIndex* h, int64_t nq, int q_dtype, int k) {
         if ((e = hipHostMalloc((void**)&h->ghI, nd * 8, hipHostMallocDefault)) != hipSuccess) return e;
         h->ghd_n = nd;
     }
-    if (!h->ghnf && (e = hipHostMalloc((void**)&h->ghnf, 4, hipHostMallocDefault)) != hipSuccess) return e;
+    if (!h->ghnf && (e = hipHostMalloc((void**)&h->ghnf, 8, hipHostMallocDefault)) != hipSuccess) return e;
     SearchPlan P;
     if ((e = plan_search(h, nq, h->qin.p, q_dtype, k, (float*)h->dws.p, (int64_t*)h->iws.p, P)) != hipSuccess)
         return e;
@@ -682,6 +777,7 @@ hipError_t graph_build(FxIndex* h, int64_t nq, int q_dtype, int k) {
     if (ce == hipSuccess) ce = hipMemcpyAsync(h->ghD, P.rp.D, nd * 4, hipMemcpyDeviceToHost, s);
     if (ce == hipSuccess) ce = hipMemcpyAsync(h->ghI, P.rp.I, nd * 8, hipMemcpyDeviceToHost, s);
     if (ce == hipSuccess) ce = hipMemcpyAsync(h->ghnf, P.rp.n_flag, 4, hipMemcpyDeviceToHost, s);
+    if (ce == hipSuccess) ce = hipMemcpyAsync(h->ghnf + 1, P.n_exact, 4, hipMemcpyDeviceToHost, s);
     g_graph_capture = false;
     hipGraph_t graph = nullptr;
     e = hipStreamEndCapture(s, &graph);  // always end the capture: the stream must leave capture mode
@@ -709,7 +805,8 @@ int graph_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int k, floa
         HIP_TRY(hipStreamSynchronize(s));
         memcpy(D, h->ghD, (size_t)nq * k * 4);
         memcpy(I, h->ghI, (size_t)nq * k * 8);
-        h->last_fallbacks = *h->ghnf;
+        h->last_fallbacks = h->ghnf[0];
+        h->last_exact = h->ghnf[1];
         h->fb_pending = false;
         return FX_OK;
     }
@@ -791,7 +888,8 @@ void fx_index_free(FxIndex* h) {
         for (DevBuf* b : {&h->qin, &h->qf32, &h->qop, &h->qeps, &h->cand_d, &h->cand_i, &h->dws, &h->iws, &h->flag,
                           &h->fbc_d, &h->fbc_i, &h->stage, &h->gtau, &h->trace, &h->dbgbuf, &h->split, &h->cnorms,
                           &h->centre, &h->mu_part, &h->qshift, &h->qrho, &h->stamps, &h->pub, &h->cand2_d,
-                          &h->cand2_i})
+                          &h->cand2_i, &h->rq_f32, &h->rq_op, &h->rq_eps, &h->rq_rho, &h->rq_shift, &h->rq_gtau,
+                          &h->rq_cand_d, &h->rq_cand_i, &h->rq_flag})
             b->release();
         graph_release(h);
         if (h->ghq) (void)hipHostFree(h->ghq);
@@ -933,6 +1031,7 @@ int fx_index_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_me
             HIP_TRY(hipMemsetAsync(I, 0xff, (size_t)nq * k * 8, h->stream()));
         }
         h->last_fallbacks = 0;
+        h->last_exact = 0;
         h->fb_pending = false;
         return FX_OK;
     }
@@ -943,16 +1042,34 @@ int fx_index_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_me
     return do_search(h, nq, q, q_dtype, q_mem, k, D, I, out_mem);
 }
 
+// the counts of the last search (after a device-resident one: synchronises the
+// index stream, which is ordered after every stream the index used before)
+static int read_counts(FxIndex* h) {
+    if (h->fb_pending) {
+        DeviceGuard g(h->device);
+        HIP_TRY(hipStreamSynchronize(h->stream()));
+        h->last_fallbacks = h->pin_nf[0];
+        h->last_exact = h->pin_nf[1];
+        h->fb_pending = false;
+    }
+    return FX_OK;
+}
+
 int fx_index_last_fallbacks(FxIndex* h, int64_t* out) {
     if (!h || !out) return set_err(FX_E_ARG, "null argument");
     std::lock_guard<std::mutex> lk(h->mu);
-    if (h->fb_pending) {  // a device-resident search left its count in flight
-        DeviceGuard g(h->device);
-        HIP_TRY(hipStreamSynchronize(h->stream()));
-        h->last_fallbacks = *h->pin_nf;
-        h->fb_pending = false;
-    }
+    const int rc = read_counts(h);
+    if (rc != FX_OK) return rc;
     *out = h->last_fallbacks;
+    return FX_OK;
+}
+
+int fx_index_last_exact_fallbacks(FxIndex* h, int64_t* out) {
+    if (!h || !out) return set_err(FX_E_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(h->mu);
+    const int rc = read_counts(h);
+    if (rc != FX_OK) return rc;
+    *out = h->last_exact;
     return FX_OK;
 }
 

@@ -67,6 +67,8 @@ struct ScanParams {
                                 // last compacted top-KP keys per query (null: not used)
     unsigned long long* stamps; // diagnostics only (FX_SCAN_STAMPS, -DFX_ABLATION builds):
                                 // [grid][4 waves][16] per-wave cycle sums of the scan's phases
+    const int* nq_dev;          // non-null (the re-scan of uncertified queries): the live query
+                                // count is min(*nq_dev, nq), known only on the device
 };
 
 // queries are zero-padded to a multiple of QPAD (the scan's query tile)
@@ -96,6 +98,9 @@ struct RefineParams {
     int force_fb;          // test hook (FX_FORCE_FALLBACK=1): flag every query -> exact fallback
     const unsigned* gtau;  // k <= KP: the scan's final shared thresholds (ordered bits): every row a split
                            // dropped lies above it, so it caps the certification bound; null: unused
+    const int* nq_dev;     // non-null: live query count min(*nq_dev, nq) (the re-scan)
+    const int* out_idx;    // non-null: query q's results go to row out_idx[q] of D / I, and an
+                           // uncertified q is flagged as out_idx[q] (the re-scan's gathered queries)
 };
 
 // exact fallback (k_fb_scan / k_fb_merge): corpus splits per flagged query,
@@ -136,6 +141,8 @@ struct PrepParams {
     const unsigned* mbits;     // max |y|^2 of the stored rows (float bits)
     const unsigned* img_bits;  // max srcC of the scan image (= mbits without an image)
     const float* mu;        // centre of the scan image (null: none)
+    const int* qidx;        // non-null: row r of the batch is row qidx[r] of q (the re-scan's gather)
+    const int* nq_dev;      // non-null: live query count min(*nq_dev, nq); later rows are padding
 };
 hipError_t launch_prep_queries(const PrepParams& p, hipStream_t s);
 hipError_t launch_scan(int st_dt, int metric, const ScanParams& p, hipStream_t s);

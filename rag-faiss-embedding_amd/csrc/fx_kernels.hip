@@ -459,14 +459,16 @@ __global__ __launch_bounds__(256) void k_prep_queries(PrepParams p, double gamma
     const int lane = threadIdx.x & 63;
     const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= p.nq_pad) return;
-    const bool live = r < p.nq;
+    const int64_t nq = p.nq_dev ? min((int64_t)*p.nq_dev, p.nq) : p.nq;
+    const bool live = r < nq;
+    const int64_t src = live && p.qidx ? (int64_t)p.qidx[r] : r;  // source row of q
     const int kdim = p.kdim;
     const float scale = p.metric == L2 ? -2.0f : -1.0f;
     // xn2 |x|^2, sc |x - mu|^2 (F32S), on2 |op|^2, rr |r|^2, rx r.x, mn2 |mu|^2
     double xn2 = 0.0, sc = 0.0, on2 = 0.0, rr = 0.0, rx = 0.0, mn2 = 0.0;
     bool bad = false;
     for (int c = lane; c < kdim; c += 64) {
-        const float v = (live && c < p.d) ? load_elem(p.q, r * p.d + c, p.q_dt) : 0.0f;
+        const float v = (live && c < p.d) ? load_elem(p.q, src * p.d + c, p.q_dt) : 0.0f;
         p.qf32[r * (int64_t)kdim + c] = v;
         const float m = p.mu ? p.mu[c] : 0.0f;
         xn2 += (double)v * (double)v;
@@ -573,7 +575,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_topk(ScanParams p) {
     const int wm = wave >> 1, wn = wave & 1;
     int qtile, split;
     map_block(blockIdx.x, p, qtile, split);
-    if (qtile >= p.n_qtiles) return;
+    const int64_t nq = p.nq_dev ? min((int64_t)*p.nq_dev, p.nq) : p.nq;
+    if (qtile >= p.n_qtiles || (int64_t)qtile * TILE_Q >= nq) return;
     const int ct0 = (int)((int64_t)split * p.n_ctiles / p.splits);
     const int ct1 = (int)((int64_t)(split + 1) * p.n_ctiles / p.splits);
     const int nks = p.row_bytes / STAGE_B;
@@ -661,7 +664,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_topk(ScanParams p) {
 #pragma unroll
             for (int n = 0; n < 4; ++n) {
                 qloc[n] = wn * 64 + n * 16 + (lane & 15);
-                qv[n] = q0 + qloc[n] < p.nq;
+                qv[n] = q0 + qloc[n] < nq;
                 tn[n] = tau[qloc[n]];
                 pend[n] = 0u;
             }
@@ -737,7 +740,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_topk(ScanParams p) {
     __syncthreads();
     const int64_t obase = ((int64_t)qtile * p.splits + split) * TILE_Q;
     for (int q = wave; q < TILE_Q; q += 4) {
-        if (q0 + q >= p.nq) break;
+        if (q0 + q >= nq) break;
         const int c = min(cnt[q], CAP);
         float d = lane < c ? lst_d[q * CAP + lane] : FX_INF;
         int i = lane < c ? lst_i[q * CAP + lane] : INT_MAX;
@@ -1003,7 +1006,8 @@ __global__ __launch_bounds__(BT_THREADS) void k_refine_big(RefineParams p) {
     __shared__ BtState<int> st;
     __shared__ unsigned t_split;
     const int64_t q = blockIdx.x;
-    if (q >= p.nq) return;
+    if (q >= (p.nq_dev ? min((int64_t)*p.nq_dev, p.nq) : p.nq)) return;
+    const int64_t oq = p.out_idx ? (int64_t)p.out_idx[q] : q;  // output row (the re-scan scatters)
     const int tid = threadIdx.x;
     const int qtile = (int)(q / TILE_Q), qq = (int)(q % TILE_Q);
     const int K1 = p.k1, B = bt_cap(K1);
@@ -1058,8 +1062,8 @@ __global__ __launch_bounds__(BT_THREADS) void k_refine_big(RefineParams p) {
     // phase 3: top-k out (faiss padding past the candidates), certification
     for (int t = tid; t < p.k; t += BT_THREADS) {
         const bool valid = t < n1;
-        p.D[q * p.k + t] = valid ? (METRIC == L2 ? ed[t] : -ed[t]) : (METRIC == L2 ? FLT_MAX : -FLT_MAX);
-        p.I[q * p.k + t] = valid ? (int64_t)ei[t] + p.id_offset : (int64_t)-1;
+        p.D[oq * p.k + t] = valid ? (METRIC == L2 ? ed[t] : -ed[t]) : (METRIC == L2 ? FLT_MAX : -FLT_MAX);
+        p.I[oq * p.k + t] = valid ? (int64_t)ei[t] + p.id_offset : (int64_t)-1;
     }
     if (tid == 0) {
         bool ok;
@@ -1070,7 +1074,7 @@ __global__ __launch_bounds__(BT_THREADS) void k_refine_big(RefineParams p) {
         }
         if (!ok || p.force_fb) {
             const int pos = atomicAdd(p.n_flag, 1);
-            p.flag_list[pos] = (int)q;
+            p.flag_list[pos] = (int)oq;
         }
     }
 }
@@ -1381,7 +1385,7 @@ hipError_t launch_scan(int st_dt, int metric, const ScanParams& p, hipStream_t s
 
 template <int DT, int METRIC>
 static hipError_t refine_t(const RefineParams& p, hipStream_t s) {
-    if (p.k > KP)
+    if (p.k > KP || p.k1 > 0)  // (k1 > 0 with k <= KP: the re-scan's wide candidate set)
         hipLaunchKernelGGL((k_refine_big<DT, METRIC>), dim3((unsigned)p.nq), dim3(BT_THREADS), 0, s, p);
     else if (p.prefetch > 1)
         hipLaunchKernelGGL((k_refine<DT, METRIC, 4>), dim3((unsigned)((p.nq + 3) / 4)), dim3(256), 0, s, p);

@@ -96,7 +96,9 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     int qtile, split;
     map_block(blockIdx.x, p, qtile, split);
-    if (qtile >= p.n_qtiles) return;
+    // the live query count (the re-scan of uncertified queries learns it on the device)
+    const int64_t nq = p.nq_dev ? min((int64_t)*p.nq_dev, p.nq) : p.nq;
+    if (qtile >= p.n_qtiles || (int64_t)qtile * TILE_Q >= nq) return;
     const int ct0 = (int)((int64_t)split * p.n_ctiles / p.splits);
     const int ct1 = (int)((int64_t)(split + 1) * p.n_ctiles / p.splits);
     const int ntiles = ct1 - ct0;
@@ -187,7 +189,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
     int qloc[N];
 #pragma unroll
     for (int n = 0; n < N; ++n) qloc[n] = qw0 + n * 16 + (lane & 15);
-    const bool qv0 = q0 + qloc[0] < p.nq, qv1 = q0 + qloc[1] < p.nq;
+    const bool qv0 = q0 + qloc[0] < nq, qv1 = q0 + qloc[1] < nq;
     // per-lane LDS addresses: my two queries' list rows, my thresholds in a norm slot
     const uint32_t lq[N] = {ld_off + (uint32_t)(qloc[0] * CAP * 4), ld_off + (uint32_t)(qloc[1] * CAP * 4)};
     const uint32_t li_d = li_off - ld_off;
@@ -487,7 +489,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
     const int64_t obase = ((int64_t)qtile * p.splits + split) * TILE_Q;
     for (int qi = 0; qi < 32; ++qi) {
         const int q = qw0 + qi;
-        if (q0 + q >= p.nq) break;
+        if (q0 + q >= nq) break;
         const int cq = qi < 16 ? __builtin_amdgcn_readlane(lr.cnt[0], qi) : __builtin_amdgcn_readlane(lr.cnt[1], qi - 16);
         const int cn = min(cq, CAP);
         float d = lane < cn ? lst_d[q * CAP + lane] : FX_INF;
@@ -515,6 +517,7 @@ static hipError_t scan_v4_t(const ScanParams& p, hipStream_t s) {
     if constexpr (ABL == 0 && DT == BF16 && METRIC == L2 && KSTEPS == 24) {
         switch (p.dbg & 2047) {
             case 1: return scan_v4_t<DT, METRIC, KSTEPS, 1, LN>(p, s);
+            case 9: return scan_v4_t<DT, METRIC, KSTEPS, 9, LN>(p, s);
             case 2: return scan_v4_t<DT, METRIC, KSTEPS, 2, LN>(p, s);
             case 4: return scan_v4_t<DT, METRIC, KSTEPS, 4, LN>(p, s);
             case 8: return scan_v4_t<DT, METRIC, KSTEPS, 8, LN>(p, s);

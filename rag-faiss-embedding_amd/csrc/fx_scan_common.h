@@ -13,15 +13,6 @@ namespace fx {
 // padding rows (|y|^2 = +inf -> key +inf) never do.
 constexpr float KEY_MAX = FLT_MAX;
 
-template <int... Is, typename F>
-__device__ __forceinline__ void static_for_impl(std::integer_sequence<int, Is...>, F&& f) {
-    (f(std::integral_constant<int, Is>{}), ...);
-}
-template <int N, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-    static_for_impl(std::make_integer_sequence<int, N>{}, f);
-}
-
 // one 1 KiB LDS-DMA piece: lane l moves 16 B from sbase + voff + OFF to
 // LDS[lds + 16 l].  The instruction offset is added to the LDS address as
 // well (LDS = M0 + OFF + 16 lane), so M0 is set to lds - OFF (>= 0: the ring
@@ -84,11 +75,11 @@ __device__ __forceinline__ unsigned union_kth_v(const unsigned (&kv)[4], unsigne
 #pragma unroll
     for (int i = 0; i < 4; ++i) lo = kv[i] < lo ? kv[i] : lo;
     // wave minimum: the answer lies in [lo, hi]
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const unsigned t = __shfl_xor(lo, o, 64);
+    const int lane = __lane_id();
+    static_for<6>([&](auto T) {
+        const unsigned t = (unsigned)lane_xor<(32 >> decltype(T)::value)>((int)lo, lane);
         lo = t < lo ? t : lo;
-    }
+    });
     for (int it = 0; it < 8 && lo < hi; ++it) {
         const unsigned mid = lo + (hi - lo) / 2;
         int c = 0;
@@ -115,22 +106,6 @@ __device__ __forceinline__ void ds_wr32(uint32_t off, int v) {
 // and rows); its entry count and its pruning threshold live in registers
 // (cntv[n], tauv[n]), the same value in the 4 lanes that hold the query, so a
 // push reserves its slots without an LDS atomic round trip.
-
-// x of lane ^ 16 / lane ^ 32 without the LDS crossbar: gfx950's
-// v_permlane16_swap (odd 16-lane rows of the first operand <-> even rows of
-// the second) and v_permlane32_swap (upper half of the first <-> lower half of
-// the second) on two copies of x.  The s_nop covers a VALU write of the
-// copies just before (inline asm is not padded by the compiler).
-__device__ __forceinline__ int lane_xor16(int x, int lane) {
-    int a = x, b = x;
-    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
-    return (lane & 16) ? a : b;
-}
-__device__ __forceinline__ int lane_xor32(int x, int lane) {
-    int a = x, b = x;
-    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
-    return (lane & 32) ? a : b;
-}
 
 // Exclusive prefix and total of `c` over the 4 lanes that hold one query
 // (lane >> 4 = 0..3, the same lane & 15).

@@ -181,9 +181,17 @@ class _FlatIndex:
         return Dp, Ip
 
     def last_fallbacks(self) -> int:
-        """Queries of the last search re-ranked by the exact fallback scan."""
+        """Queries of the last search whose top-k the scan's candidates could
+        not certify (re-scanned with a wide candidate set)."""
         v = ctypes.c_int64(0)
         check(lib.fx_index_last_fallbacks(self._h, ctypes.byref(v)))
+        return v.value
+
+    def last_exact_fallbacks(self) -> int:
+        """Of those, the queries the re-scan could not certify either,
+        re-ranked by the exact fp64 scan of every row."""
+        v = ctypes.c_int64(0)
+        check(lib.fx_index_last_exact_fallbacks(self._h, ctypes.byref(v)))
         return v.value
 
     def reset(self) -> None:

@@ -99,13 +99,14 @@ def test_k_beyond_ntotal_pads(fx):
 
 @pytest.mark.parametrize("k", [10, 100])
 def test_forced_fallback_is_exact(fx, gauss, monkeypatch, k):
-    """Every query through the device-gated exact fallback: same results."""
+    """Every query through the device-gated exact fallback (force_fallback 2:
+    past the re-scan too): same results."""
     xb, xq = gauss
     ix = fx.IndexFlatL2(384)
     ix.add(xb[:100_000])
-    ix.set_option("force_fallback", 1)
+    ix.set_option("force_fallback", 2)
     D, I = ix.search(xq, k)
-    assert ix.last_fallbacks() == len(xq)
+    assert ix.last_fallbacks() == len(xq) and ix.last_exact_fallbacks() == len(xq)
     Dr, Ir = C.knn_exact(xq, xb[:100_000], k)
     assert_parity(D, I, Dr, Ir)
 
@@ -118,9 +119,9 @@ def test_forced_fallback_many_queries(fx, monkeypatch):
     xq = rng.standard_normal((5000, 64)).astype(np.float32)
     ix = fx.IndexFlatL2(64)
     ix.add(xb)
-    ix.set_option("force_fallback", 1)
+    ix.set_option("force_fallback", 2)
     D, I = ix.search(xq, 7)
-    assert ix.last_fallbacks() == 5000
+    assert ix.last_fallbacks() == 5000 and ix.last_exact_fallbacks() == 5000
     Dr, Ir = C.knn_exact(xq, xb, 7)
     assert_parity(D, I, Dr, Ir)
 

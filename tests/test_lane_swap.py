@@ -33,15 +33,23 @@ def test_lane_swaps_on_device():
     if not LIB.exists():
         pytest.fail(f"{LIB} missing: build it on the CPU first (tests/test_lane_swap.py::test_probe_builds)")
     lib = ctypes.CDLL(str(LIB))
-    out = np.zeros((4, 64), dtype=np.int32)
-    rc = lib.lane_probe(out.ctypes.data_as(ctypes.c_void_p))
+    rng = np.random.default_rng(4)
+    keys = rng.integers(0, 9, 64).astype(np.float32)           # many duplicate keys: ties -> smaller id
+    keys[rng.integers(0, 64, 5)] = np.inf
+    out = np.zeros((9, 64), dtype=np.int32)
+    kout = np.zeros(64, dtype=np.float32)
+    rc = lib.lane_probe(keys.ctypes.data_as(ctypes.c_void_p), out.ctypes.data_as(ctypes.c_void_p),
+                        kout.ctypes.data_as(ctypes.c_void_p))
     assert rc == 0
     x = (np.arange(64) * 7 + 3) % 11
     lane = np.arange(64)
-    assert (out[0] == x[lane ^ 16]).all(), out[0]
-    assert (out[1] == x[lane ^ 32]).all(), out[1]
+    for row, s in enumerate((1, 2, 4, 8, 16, 32)):
+        assert (out[row] == x[lane ^ s]).all(), (s, out[row])
     # quad prefix over lanes l & 15 + 16 j, j = 0..3
     ex = np.array([x[[(l & 15) + 16 * j for j in range(l >> 4)]].sum() for l in lane])
     tot = np.array([x[[(l & 15) + 16 * j for j in range(4)]].sum() for l in lane])
-    assert (out[2] == ex).all(), out[2]
-    assert (out[3] == tot).all(), out[3]
+    assert (out[6] == ex).all(), out[6]
+    assert (out[7] == tot).all(), out[7]
+    ids = (lane * 37) % 64
+    order = sorted(range(64), key=lambda j: (keys[j], ids[j]))
+    assert (kout == keys[order]).all() and (out[8] == ids[order]).all()

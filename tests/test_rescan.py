@@ -1,0 +1,89 @@
+"""The re-scan of uncertified queries (fx_index.cpp plan_rescan): queries
+whose top-k the scan's KP-candidate lists cannot certify are scanned again
+with a wide candidate set (k_refine_big over k1 = max(512, 4k) candidates)
+before anything falls to the exact fp64 scan of every row.
+
+Case built to need it: a shell of 100 rows whose distances to the query lie
+within the scan's error bound of each other (relative spacing 1e-6, bound
+~1e-4), everything else far away.  Pass 1's 32 candidates cannot separate the
+k-th from the rows it dropped; the re-scan's 512 candidates reach past the
+shell and certify.  Ids must stay oracle-exact either way."""
+import numpy as np
+import pytest
+
+from oracle import cpu as C
+from tests.test_gpu_parity import assert_parity
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def fx():
+    from rag_faiss_embedding_amd import _lib, faiss
+    if _lib.device_count() == 0:
+        pytest.fail("no GPU visible: -m gpu tests must run on the MI355X box")
+    return faiss
+
+
+def shell_corpus(n=60_000, d=384, shell=100, seed=3):
+    rng = np.random.default_rng(seed)
+    u = rng.standard_normal((n, d))
+    u /= np.linalg.norm(u, axis=1, keepdims=True)
+    r = np.full(n, 2.0)
+    r[:shell] = np.sqrt(1.0 + 1e-6 * np.arange(shell))   # |y|^2 = 1 + 1e-6 i
+    rng.shuffle(r)
+    return (u * r[:, None]).astype(np.float32)
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16", "float16"])
+@pytest.mark.parametrize("k", [10, 32])
+def test_shell_rescan_certifies(fx, dtype, k):
+    xb = shell_corpus()
+    xq = np.zeros((8, xb.shape[1]), dtype=np.float32)
+    xq[:, 0] = np.float32(1e-4) * np.arange(8, dtype=np.float32)  # near the origin: the shell is equidistant
+    ix = fx.IndexFlatL2(xb.shape[1], dtype=dtype)
+    ix.add(xb)
+    D, I = ix.search(xq, k)
+    ref = xb if dtype == "float32" else ix.reconstruct_n(0, len(xb))
+    Dr, Ir = C.knn_exact(xq, ref, k)
+    assert_parity(D, I, Dr, Ir)
+    n1, n2 = ix.last_fallbacks(), ix.last_exact_fallbacks()
+    print(f"\n[rescan] {dtype} k={k}: re-scanned {n1}/8, exact {n2}/8")
+    if dtype == "float32":
+        assert n1 > 0, "the shell case should defeat the scan's 32-candidate certification"
+    assert n2 == 0, "the re-scan's wide candidate set should certify the shell"
+
+
+@pytest.mark.parametrize("k", [5, 100])
+def test_forced_levels(fx, k):
+    """force_fallback = 1: every query through the re-scan; = 2: every query
+    through the re-scan AND the exact scan.  Results identical and exact."""
+    rng = np.random.default_rng(9)
+    xb = rng.standard_normal((20_000, 128)).astype(np.float32)
+    xq = rng.standard_normal((300, 128)).astype(np.float32)
+    Dr, Ir = C.knn_exact(xq, xb, k)
+    for level in (0, 1, 2):
+        ix = fx.IndexFlatL2(128)
+        ix.add(xb)
+        ix.set_option("force_fallback", level)
+        D, I = ix.search(xq, k)
+        assert_parity(D, I, Dr, Ir)
+        assert ix.last_fallbacks() == (0 if level == 0 else len(xq))
+        assert ix.last_exact_fallbacks() == (len(xq) if level == 2 else 0)
+
+
+def test_rescan_device_resident(fx):
+    """The re-scan is decided on the device: a device-resident search with
+    every query forced through it returns exact results stream-ordered."""
+    import torch
+    rng = np.random.default_rng(10)
+    xb = rng.standard_normal((30_000, 256)).astype(np.float32)
+    xq = rng.standard_normal((700, 256)).astype(np.float32)
+    ix = fx.IndexFlatL2(256, dtype="bfloat16")
+    ix.add(torch.from_numpy(xb).cuda())
+    ix.set_option("force_fallback", 1)
+    D, I = ix.search(torch.from_numpy(xq).cuda(), 10)
+    torch.cuda.synchronize()
+    Dr, Ir = C.knn_exact(xq, ix.reconstruct_n(0, len(xb)), 10)
+    assert_parity(D.cpu().numpy(), I.cpu().numpy(), Dr, Ir)
+    assert ix.last_fallbacks() == len(xq) and ix.last_exact_fallbacks() == 0

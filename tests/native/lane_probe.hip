@@ -1,9 +1,9 @@
 // Probe of the VALU cross-lane helpers of the scan and the refine
-// (fx_device.h lane_xor<S>, sort64; fx_scan_common.h quad_prefix), checked
+// (fx_device.h lane_xor<S>, sort64), checked
 // against their definitions by tests/test_lane_swap.py.
 #include "fx_scan_common.h"
 
-// out[0 .. 6*64): lane_xor<1..32>(x); then quad prefix excl / total; then a
+// out[0 .. 6*64): lane_xor<1..32>(x); then lane ^ 48, lane ^ 7; then a
 // sort64 of (key, id) with duplicate keys: keys and ids
 __global__ void k_lane_probe(const float* keys_in, int* out, float* keys_out) {
     const int lane = threadIdx.x & 63;
@@ -14,10 +14,9 @@ __global__ void k_lane_probe(const float* keys_in, int* out, float* keys_out) {
     out[3 * 64 + lane] = fx::lane_xor<8>(x, lane);
     out[4 * 64 + lane] = fx::lane_xor<16>(x, lane);
     out[5 * 64 + lane] = fx::lane_xor<32>(x, lane);
-    int ex, tot;
-    fx::quad_prefix(x, lane, ex, tot);
-    out[6 * 64 + lane] = ex;
-    out[7 * 64 + lane] = tot;
+    // lane ^ 48 and lane ^ 7 as compositions
+    out[6 * 64 + lane] = fx::lane_xor<16>(fx::lane_xor<32>(x, lane), lane);
+    out[7 * 64 + lane] = fx::lane_xor<1>(fx::lane_xor<2>(fx::lane_xor<4>(x, lane), lane), lane);
     float d = keys_in[lane];
     int i = (lane * 37) % 64;
     fx::sort64(d, i, lane);

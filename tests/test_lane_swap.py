@@ -1,7 +1,8 @@
-"""gfx950 cross-lane helpers of the scan's list pushes (fx_scan_common.h
-lane_xor16 / lane_xor32 / quad_prefix, built on v_permlane16_swap and
-v_permlane32_swap): checked on the device against their definition, through a
-small probe kernel compiled with the same header (hipcc, gfx950)."""
+"""gfx950 VALU cross-lane helpers of the scan and the refine (fx_device.h
+lane_xor<S>: DPP quad_perm / row_ror inside 16-lane rows, v_permlane16_swap
+and v_permlane32_swap across them; the bitonic sort64 built on them): checked
+on the device against their definition, through a small probe kernel compiled
+with the same headers (hipcc, gfx950)."""
 import ctypes
 import subprocess
 from pathlib import Path
@@ -45,11 +46,8 @@ def test_lane_swaps_on_device():
     lane = np.arange(64)
     for row, s in enumerate((1, 2, 4, 8, 16, 32)):
         assert (out[row] == x[lane ^ s]).all(), (s, out[row])
-    # quad prefix over lanes l & 15 + 16 j, j = 0..3
-    ex = np.array([x[[(l & 15) + 16 * j for j in range(l >> 4)]].sum() for l in lane])
-    tot = np.array([x[[(l & 15) + 16 * j for j in range(4)]].sum() for l in lane])
-    assert (out[6] == ex).all(), out[6]
-    assert (out[7] == tot).all(), out[7]
+    assert (out[6] == x[lane ^ 48]).all(), out[6]
+    assert (out[7] == x[lane ^ 7]).all(), out[7]
     ids = (lane * 37) % 64
     order = sorted(range(64), key=lambda j: (keys[j], ids[j]))
     assert (kout == keys[order]).all() and (out[8] == ids[order]).all()

@@ -269,9 +269,12 @@ void plan_scan(const FxIndex* h, int64_t nq, int k, ScanParams& p) {
     constexpr int min_tiles = 4;
     // placement (map_tile): corpus-partitioned by default (config (d): 257 vs
     // 742 GB fetched past L2 per launch, ~2 % faster); scan_place = 0 forces
-    // the query-tile groups of round 1
+    // the query-tile groups of round 1.  Also for fewer than 8 query tiles:
+    // the ntl blocks of one split then run side by side on one XCD, so the
+    // split is fetched past L2 once for all of them (nq = 256: once instead
+    // of twice)
     const int place = h->opt.place >= 0 ? h->opt.place : 1;
-    if (place == 1 && ntl >= 8 && nct >= 8 * min_tiles) {
+    if (place == 1 && nct >= 8 * min_tiles) {
         // XCD x owns 1/8 of the corpus for every query tile; sx splits per
         // XCD so that its ntl * sx blocks fill whole rounds of its 32 CUs
         p.place = 1;
@@ -279,7 +282,7 @@ void plan_scan(const FxIndex* h, int64_t nq, int k, ScanParams& p) {
         const int max_sx = std::max(1, nct / (8 * min_tiles));
         int best = 1;
         double best_eff = 0.0;
-        for (int sx = 1; sx <= std::min(max_sx, 16); ++sx) {
+        for (int sx = 1; sx <= std::min(max_sx, std::max(16, 128 / ntl)); ++sx) {
             const double live = (double)ntl * sx;
             const double eff = live / (std::ceil(live / 32.0) * 32.0);
             if (eff > best_eff + 1e-9) { best_eff = eff; best = sx; }

@@ -265,7 +265,10 @@ def cpu_baseline_and_recall(args, n_total, d, dtype, k, D, I, xq_dev, nthreads, 
 def read_pmc_traffic(cfg_name, n_local, nq, data="synthetic"):
     """HBM bytes per scan launch from a committed rocprofv3 --pmc summary of
     this same workload (profiles/pmc_scan_<cfg>[_clustered].json), or None."""
-    p = ROOT / "profiles" / f"pmc_scan_{cfg_name}{'' if data == 'synthetic' else '_' + data}.json"
+    base = f"pmc_scan_{cfg_name}{'' if data == 'synthetic' else '_' + data}"
+    p = ROOT / "profiles" / f"{base}_nq{nq}.json"  # a small-batch sweep point
+    if not p.exists():
+        p = ROOT / "profiles" / f"{base}.json"
     if not p.exists():
         return None
     try:

@@ -444,10 +444,14 @@ template <> struct AsmMmaV<F32> {
     }
 };
 
-// 48 wait states: covers the XDL-write -> VALU-read distance of the slowest
-// scan MFMA (16x16x4 f32 chain, 40-cycle dependent latency)
+// 20 wait states before a VALU reads the accumulators: the XDL-write ->
+// VALU-read requirement is (passes + 3) wait states, 19 for the longest
+// (16-pass) MFMA; the scan's MFMAs have at most 8 passes, and the epilogue
+// reads the last-written accumulators (acc[7][*]) only after 14 further VALU
+// instructions.  (Was 48: each s_nop state costs a 4-cycle issue slot, so the
+// pad cost ~190 cycles per tile.)
 __device__ __forceinline__ void acc_fence_v(f32x4 (&acc)[8][2]) {
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7"
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3"
                  : "+v"(acc[0][0]), "+v"(acc[0][1]), "+v"(acc[1][0]), "+v"(acc[1][1]), "+v"(acc[2][0]),
                    "+v"(acc[2][1]), "+v"(acc[3][0]), "+v"(acc[3][1]), "+v"(acc[4][0]), "+v"(acc[4][1]),
                    "+v"(acc[5][0]), "+v"(acc[5][1]), "+v"(acc[6][0]), "+v"(acc[6][1]), "+v"(acc[7][0]),

@@ -92,6 +92,8 @@ struct Options {
     int centre = 1;          // FX_CENTER: L2 scan images are centred on a row sample's mean
     int pub = 1;             // FX_SCAN_PUB: union threshold over published per-split lists
     int prune_rank = 0;      // FX_PRUNE_RANK: rank of the shared threshold (0: max(2k, 16))
+    int compact_at = 0;      // FX_COMPACT_AT: list fill that triggers a compaction (0: default, KP < v <= CAP)
+    int union_w = 0;         // FX_UNION_W: splits per union-bound window (16, 32, 64; 0: by split count)
     int scan_dbg = 0;        // FX_SCAN_DBG: ablation switches of -DFX_ABLATION builds / key dump (32)
     int graph_verbose = 0;   // FX_SEARCH_GRAPH_VERBOSE
     std::string trace, stamps, cand, keys;  // FX_SCAN_TRACE / _STAMPS / _CAND / _KEYS dump paths
@@ -112,6 +114,8 @@ struct Options {
         num("FX_CENTER", centre);
         num("FX_SCAN_PUB", pub);
         num("FX_PRUNE_RANK", prune_rank);
+        num("FX_COMPACT_AT", compact_at);
+        num("FX_UNION_W", union_w);
         num("FX_SCAN_DBG", scan_dbg);
         num("FX_SEARCH_GRAPH_VERBOSE", graph_verbose);
         str("FX_SCAN_TRACE", trace);
@@ -121,9 +125,9 @@ struct Options {
     }
     int* find(const char* name) {
         static const char* names[] = {"search_graph", "force_fallback", "scan_place", "scan_sx", "reduce_cand",
-                                      "f32_split", "centre", "scan_pub", "prune_rank", "scan_dbg"};
+                                      "f32_split", "centre", "scan_pub", "prune_rank", "scan_dbg", "compact_at", "union_w"};
         int* slots[] = {&search_graph, &force_fallback, &place, &sx, &reduce_cand,
-                        &f32_split, &centre, &pub, &prune_rank, &scan_dbg};
+                        &f32_split, &centre, &pub, &prune_rank, &scan_dbg, &compact_at, &union_w};
         for (int i = 0; i < (int)(sizeof(names) / sizeof(names[0])); ++i)
             if (strcmp(name, names[i]) == 0) return slots[i];
         return nullptr;
@@ -264,7 +268,9 @@ void plan_scan(const FxIndex* h, int64_t nq, int k, ScanParams& p) {
     p.sx = 0;
     p.pub = nullptr;
     p.prune_rank = KP;
+    p.compact_at = h->opt.compact_at > KP && h->opt.compact_at <= CAP ? h->opt.compact_at : CAP;
     p.share = k <= KP ? 1 : 0;
+    p.union_w = 16;
     const int ntl = p.n_qtiles, nct = p.n_ctiles;
     constexpr int min_tiles = 4;
     // placement (map_tile): corpus-partitioned by default (config (d): 257 vs
@@ -293,13 +299,17 @@ void plan_scan(const FxIndex* h, int64_t nq, int k, ScanParams& p) {
         p.sx = best;
         p.splits = 8 * best;
         p.grid = 8 * ntl * best;
-        return;
+    } else {
+        p.qt_per_xcd = ntl >= 8 ? (ntl + 7) / 8 : 0;
+        const int eff_q = p.qt_per_xcd > 0 ? 8 * p.qt_per_xcd : ntl;
+        p.splits = fill_splits(ntl, eff_q, nct, min_tiles);
+        if (k > KP) p.splits = std::max(p.splits, std::min(std::max(1, nct / min_tiles), (k + 3) / 4));
+        p.grid = eff_q * p.splits;
     }
-    p.qt_per_xcd = ntl >= 8 ? (ntl + 7) / 8 : 0;
-    const int eff_q = p.qt_per_xcd > 0 ? 8 * p.qt_per_xcd : ntl;
-    p.splits = fill_splits(ntl, eff_q, nct, min_tiles);
-    if (k > KP) p.splits = std::max(p.splits, std::min(std::max(1, nct / min_tiles), (k + 3) / 4));
-    p.grid = eff_q * p.splits;
+    // union-bound window (compact_regs): as many splits as there are, up to
+    // 64, each contributing its first 256 / window published keys
+    const int uw = h->opt.union_w;
+    p.union_w = uw == 16 || uw == 32 || uw == 64 ? uw : p.splits <= 16 ? 16 : p.splits <= 32 ? 32 : 64;
 }
 
 // k > KP: approx candidates the refine re-ranks exactly (k_refine_big)

@@ -63,6 +63,9 @@ struct ScanParams {
     int sx;                     // place 1: corpus splits per XCD (splits = 8 sx)
     int grid;                   // workgroups of the scan launch
     int prune_rank;             // rank of the union bound published to gtau (compact_wave)
+    int union_w;                // union bound window: 16, 32 or 64 splits (their first 256 / union_w keys)
+    int compact_at;             // a list is compacted once it holds this many entries (KP < v <= CAP;
+                                // the threshold only improves at a compaction)
     float* pub;                 // k_scan_v4 with share: [n_qtiles * TILE_Q][splits][KP] each split's
                                 // last compacted top-KP keys per query (null: not used)
     unsigned long long* stamps; // diagnostics only (FX_SCAN_STAMPS, -DFX_ABLATION builds):

@@ -12,6 +12,18 @@ namespace fx {
 // Largest finite float: thresholds start here, so real keys always pass and
 // padding rows (|y|^2 = +inf -> key +inf) never do.
 constexpr float KEY_MAX = FLT_MAX;
+// global-address-space float: loads through it are global_load (vmcnt only),
+// not flat (which also counts against lgkmcnt as a possible LDS access)
+typedef __attribute__((address_space(1))) float gfloat;
+typedef __attribute__((address_space(1))) unsigned guint;
+// relaxed agent-scope atomicMin through a global pointer (global_atomic_umin:
+// no lgkmcnt, so later LDS accesses do not wait for it)
+__device__ __forceinline__ void gmin_u32(unsigned* p, unsigned v) {
+    __hip_atomic_fetch_min((guint*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float readlane_f(float v, int l) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
 
 // one 1 KiB LDS-DMA piece: lane l moves 16 B from sbase + voff + OFF to
 // LDS[lds + 16 l].  The instruction offset is added to the LDS address as
@@ -150,14 +162,16 @@ __device__ __forceinline__ bool push_reg(const f32x4 (&acc)[M][N], int n, int m,
     return late != 0u;
 }
 
-// Compact this wave's full lists (cntv >= CAP) to their KP best; the list's
-// threshold becomes its rank-th key (rank = KP unless the union bound is on),
-// published to the shared per-query threshold.  Only the full lists are
-// visited.
+// Compact this wave's lists that hold `at` or more entries (KP < at <= CAP)
+// to their KP best; the list's threshold becomes its rank-th key (rank = KP
+// unless the union bound is on), published to the shared per-query threshold.
+// A list's threshold only improves here, so compacting before the list is
+// full (at < CAP) trades more compactions for fewer slow-path tiles.
 //
 // pub (k <= KP): the compacted list is also published to pub[query][split][KP],
 // and the shared threshold becomes the rank-th smallest key of the union of
-// the published lists of up to 16 splits (this one's window of 16) -- a valid
+// the published lists of the uw splits of this one's window (their first
+// 256 / uw keys each) -- a valid
 // bound on the query's global rank-th key, because every published entry is
 // the key of a distinct row of its split (a list read while its split
 // rewrites it mixes two versions of the same improving list: entry i of
@@ -172,41 +186,47 @@ struct ListRegs {
     int cnt[2];
     float tau[2];
 };
-__device__ __noinline__ ListRegs compact_regs(float* lst_d, int* lst_i, ListRegs r, unsigned* gtq, int qw0, int lane,
-                                              float* pub, int splits, int split, int rank) {
+__device__ __forceinline__ ListRegs compact_regs(float* lst_d, int* lst_i, ListRegs r, unsigned* gtq, int qw0, int lane,
+                                              float* pub, int splits, int split, int rank, int at, int uw) {
     int (&cntv)[2] = r.cnt;
     float (&tauv)[2] = r.tau;
-    const uint64_t f0 = __builtin_amdgcn_ballot_w64(lane < 16 && cntv[0] >= CAP);
-    const uint64_t f1 = __builtin_amdgcn_ballot_w64(lane < 16 && cntv[1] >= CAP);
+    const uint64_t f0 = __builtin_amdgcn_ballot_w64(lane < 16 && cntv[0] >= at);
+    const uint64_t f1 = __builtin_amdgcn_ballot_w64(lane < 16 && cntv[1] >= at);
     const uint64_t all = (f0 & 0xffffull) | ((f1 & 0xffffull) << 16);
     uint64_t full = all;
     while (full) {
         const int qi = __builtin_ctzll(full);
         full &= full - 1;
         const int q = qw0 + qi;
-        float d = lst_d[q * CAP + lane];
-        int i = lst_i[q * CAP + lane];
+        // entries past the count are stale (rows of earlier rounds: kept or
+        // dropped ones, so possibly duplicates) unless the list is full
+        const int cq = __builtin_amdgcn_readlane(qi < 16 ? cntv[0] : cntv[1], qi & 15);
+        const bool live = lane < cq;  // cq may exceed CAP (overflowed pushes wait in `pend`)
+        float d = live ? lst_d[q * CAP + lane] : FX_INF;
+        int i = live ? lst_i[q * CAP + lane] : INT_MAX;
         sort64(d, i, lane);
         if (lane < KP) {
             lst_d[q * CAP + lane] = d;
             lst_i[q * CAP + lane] = i;
         }
-        const float dr = __shfl(d, rank - 1, 64);
+        const float dr = readlane_f(d, rank - 1);
         if ((lane & 15) == (qi & 15)) {
             if (qi < 16) { tauv[0] = dr; cntv[0] = KP; }
             else { tauv[1] = dr; cntv[1] = KP; }
         }
         // published to gtau too, so the final gtau stays below every split's
         // local threshold (k_refine); null gtq: no cross-split pruning (k > KP)
-        if (gtq && lane == 0) atomicMin(gtq + qi, f2ord(dr));
+        if (gtq && lane == 0) gmin_u32(gtq + qi, f2ord(dr));
         if (pub && gtq && lane < KP)
-            __hip_atomic_store(pub + ((int64_t)qi * splits + split) * KP + lane, d, __ATOMIC_RELAXED,
+            __hip_atomic_store((gfloat*)(pub + ((int64_t)qi * splits + split) * KP + lane), d, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
     }
     if (!(pub && gtq)) return r;
-    // union bounds, up to 4 lists per memory round trip
-    const int w0 = split & ~15;
-    const int nsp = splits - w0 < 16 ? splits - w0 : 16;
+    // union bounds, up to 4 lists per memory round trip: the window holds uw
+    // splits (16, 32 or 64) and their first 256 / uw published keys (4 per lane)
+    const int le = uw >= 64 ? 2 : uw >= 32 ? 3 : 4;  // log2(entries per list)
+    const int w0 = split & ~(uw - 1);
+    const int nsp = splits - w0 < uw ? splits - w0 : uw;
     uint64_t rest = all;
     while (rest) {
         int qs[4];
@@ -216,24 +236,33 @@ __device__ __noinline__ ListRegs compact_regs(float* lst_d, int* lst_i, ListRegs
             qs[u] = rest ? __builtin_ctzll(rest) : -1;
             if (rest) rest &= rest - 1;
         }
+        // every lane loads unconditionally (absent lists read entry e of the
+        // first list and are masked after the load): a load under a lane
+        // condition becomes an exec-masked branch with its own vmcnt(0) wait,
+        // which serialised the 16 round trips
+        float raw[4][4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            const float* lists = pub + ((int64_t)(qs[u] < 0 ? 0 : qs[u]) * splits + w0) * KP;
+            const gfloat* lists = (const gfloat*)(pub + ((int64_t)(qs[u] < 0 ? 0 : qs[u]) * splits + w0) * KP);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const int l = (lane >> 4) + 4 * j, e = lane & 15;  // list l, entry e
-                kv[u][j] = (qs[u] >= 0 && l < nsp)
-                               ? f2ord(__hip_atomic_load(lists + l * KP + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                               : 0xFFFFFFFFu;
+                const int x = lane + 64 * j, l = x >> le, e = x & ((1 << le) - 1);  // list l, entry e
+                raw[u][j] = __hip_atomic_load(lists + (l < nsp ? l : 0) * KP + e, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
             }
         }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                kv[u][j] = (qs[u] >= 0 && ((lane + 64 * j) >> le) < nsp) ? f2ord(raw[u][j]) : 0xFFFFFFFFu;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             if (qs[u] < 0) break;
             const int qi = qs[u];
-            const unsigned own = f2ord(__shfl(qi < 16 ? tauv[0] : tauv[1], qi & 15, 64));
+            const unsigned own = f2ord(readlane_f(qi < 16 ? tauv[0] : tauv[1], qi & 15));
             const unsigned v = union_kth_v(kv[u], own, rank);
-            if (lane == 0 && v < own) atomicMin(gtq + qi, v);
+            if (lane == 0 && v < own) gmin_u32(gtq + qi, v);
         }
     }
     return r;

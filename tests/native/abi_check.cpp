@@ -159,6 +159,12 @@ int main() {
     n += 5;
     search_and_check(ix, xb, n, d, 1, 5, rng, "graph after add");
     OK(fx_index_set_option(ix, "search_graph", 0));
+    // list-maintenance options: any valid value keeps results exact
+    OK(fx_index_set_option(ix, "compact_at", 40));
+    OK(fx_index_set_option(ix, "union_w", 64));
+    search_and_check(ix, xb, n, d, 64, 10, rng, "compact_at 40, union window 64");
+    OK(fx_index_set_option(ix, "compact_at", 0));
+    OK(fx_index_set_option(ix, "union_w", 0));
 
     // ---- IxF2 round trip, fp32 and bf16 storage ---------------------------
     const std::string path = std::string(getenv("TMPDIR") ? getenv("TMPDIR") : "/tmp") + "/fx_abi_check.bin";

@@ -1,0 +1,52 @@
+"""The scan's list-maintenance options (fx_scan_common.h compact_regs) keep
+results exact whatever their value: the compaction trigger `compact_at`
+(a list is compacted to its KP best once it holds that many entries, 33..64)
+and the union-bound window `union_w` (16, 32 or 64 splits, each contributing
+its first 256 / union_w published keys).  Both only change how fast the
+pruning threshold falls; every dropped row still lies above the final shared
+threshold that the refine certifies against.  Checked against the oracle on
+a batch that runs many splits (short splits: cold lists, frequent
+compactions), on uniform and clustered rows."""
+import numpy as np
+import pytest
+
+from oracle import cpu as C
+from tests.test_gpu_parity import assert_parity
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def fx():
+    from rag_faiss_embedding_amd import _lib, faiss
+    if _lib.device_count() == 0:
+        pytest.fail("no GPU visible: -m gpu tests must run on the MI355X box")
+    return faiss
+
+
+def rows(kind, n, d, seed):
+    rng = np.random.default_rng(seed)
+    if kind == "uniform":
+        return rng.standard_normal((n, d)).astype(np.float32)
+    base = rng.standard_normal(d)
+    x = base / np.linalg.norm(base) + 0.05 * rng.standard_normal((n, d)) / np.sqrt(d)
+    return (x / np.linalg.norm(x, axis=1, keepdims=True)).astype(np.float32)
+
+
+@pytest.mark.parametrize("kind", ["uniform", "clustered"])
+@pytest.mark.parametrize("dtype", ["bfloat16", "float32"])
+def test_compaction_and_union_options_exact(fx, kind, dtype):
+    n, d, nq, k = 300_000, 256, 300, 10
+    xb = rows(kind, n, d, 11)
+    xq = rows(kind, nq, d, 12)
+    ix = fx.IndexFlatL2(d, dtype=dtype)
+    ix.add(xb)
+    ref = xb if dtype == "float32" else ix.reconstruct_n(0, n)
+    Dr, Ir = C.knn_exact(xq, ref, k)
+    for compact_at, union_w in [(64, 16), (40, 16), (48, 64), (33, 32), (64, 64)]:
+        ix.set_option("compact_at", compact_at)
+        ix.set_option("union_w", union_w)
+        D, I = ix.search(xq, k)
+        assert_parity(D, I, Dr, Ir)
+        print(f"\n[scan-options] {kind} {dtype} compact_at={compact_at} union_w={union_w}: "
+              f"fallbacks {ix.last_fallbacks()}/{nq}")

@@ -4,7 +4,7 @@
 # group in a pass of its own (FETCH_SIZE and WRITE_SIZE do not fit one TCC
 # pass on gfx950; no --pmc together with any trace domain), each under a hard
 # time limit (a pass over the per-block counter capacity hangs).
-# Scan variants are chosen by the caller's environment (e.g. FX_SCAN_LINE=1).
+# Scan variants are chosen by the caller's environment (FX_* options).
 # usage: tools/profile_scan.sh <tag> [bench args...]
 set -euo pipefail
 tag=$1; shift
@@ -20,6 +20,7 @@ pmc() {  # <subdir> <counters...>
 }
 pmc fetch FETCH_SIZE
 pmc write WRITE_SIZE
+if [ "${FX_PROFILE_MIN:-0}" = 1 ]; then echo "profile $tag done (trace + fetch + write)"; exit 0; fi
 pmc tcc TCC_HIT_sum TCC_MISS_sum
 pmc sq SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE
 if [ "${FX_PROFILE_EXTRA:-0}" = 1 ]; then

@@ -22,6 +22,12 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 SCAN = os.environ.get("FX_PROFILE_KERNEL", "k_scan_")  # k_scan_v4 / k_scan_q32
+RESCAN_MARK = (", 4096,", "Li4096E")  # fx_scan.hip RESCAN: the re-scan's own instance
+
+
+def is_scan(name):
+    """The main scan's launches, not the re-scan of uncertified queries."""
+    return SCAN in name and not any(m in name for m in RESCAN_MARK)
 
 
 def counters(path):
@@ -48,10 +54,10 @@ def main():
     pmc = {}
     for sub in ("fetch", "write", "tcc", "sq", "lds", "ta"):
         for name, cs in counters(prof / sub / "run_counter_collection.csv").items():
-            if SCAN in name:
+            if is_scan(name):
                 for c, vals in cs.items():
                     pmc[c] = statistics.median(vals)
-    scan_name = next(n for n in kern if SCAN in n)
+    scan_name = next(n for n in kern if is_scan(n))
     res = {"kernels": kern, "scan_kernel": scan_name, "scan_pmc_median_per_launch": pmc,
            "rows_per_gpu": rows, "nq": nq}
     if "FETCH_SIZE" in pmc:

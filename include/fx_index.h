@@ -60,10 +60,13 @@ enum {
     FX_E_OOM = -5
 };
 
-/* Maximum k served by fx_index_search (per query).  faiss's CPU
- * IndexFlatL2::search has no k cap (faiss_store.py:49,64 pass the caller's
- * k); k <= 32 takes the fused scan's fixed candidate lists, larger k a
- * block top-K refine without cross-split pruning. */
+/* Largest k served by the fused scan path (per query).  fx_index_search
+ * itself has no k cap, as faiss's IndexFlatL2::search (faiss_store.py:49,64
+ * pass the caller's k): k <= 32 takes the fused scan's fixed candidate lists,
+ * 32 < k <= FX_MAX_K a block top-K refine without cross-split pruning, and
+ * k > FX_MAX_K the exact sort path (every (query, row) distance exactly,
+ * one radix sort per query; HBM-bound, for the rare caller that asks).
+ * fx_merge_shards takes any k the same way. */
 #define FX_MAX_K 1024
 
 const char* fx_last_error(void);
@@ -112,8 +115,8 @@ int fx_index_reserve(FxIndex* index, int64_t n);
 int fx_index_add(FxIndex* index, int64_t n, const void* x, int x_dtype, int x_mem);
 
 /* index.search(x, k) (faiss_store.py:64): q[nq][d] -> D[nq][k] (f32),
- * I[nq][k] (int64), out buffers caller-allocated on out_mem.  1 <= k <=
- * FX_MAX_K.  Blocks until results are in host memory when out_mem is
+ * I[nq][k] (int64), out buffers caller-allocated on out_mem.  k >= 1 (any
+ * k; past ntotal I = -1, D = +-FLT_MAX as faiss pads).  Blocks until results are in host memory when out_mem is
  * FX_MEM_HOST; with FX_MEM_DEVICE (queries and results on the device) it
  * is stream-ordered: it enqueues its work and returns without waiting for
  * the device (the exact fallback for uncertified queries is decided on the

@@ -32,7 +32,7 @@ lib = ctypes.CDLL(str(LIB_PATH))
 F32, BF16, F16 = 0, 1, 2
 METRIC_INNER_PRODUCT, METRIC_L2 = 0, 1
 MEM_HOST, MEM_DEVICE = 0, 1
-MAX_K = 1024  # == FX_MAX_K (include/fx_index.h)
+MAX_K = 1024  # == FX_MAX_K (include/fx_index.h): largest k of the fused scan path (larger k: exact sort path)
 
 _vp = ctypes.c_void_p
 _i64 = ctypes.c_int64

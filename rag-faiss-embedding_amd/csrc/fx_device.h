@@ -54,6 +54,47 @@ __device__ __forceinline__ void store_elem(void* p, int64_t idx, int dt, float v
     else ((uint16_t*)p)[idx] = dt == BF16 ? f2bf(v) : f2h(v);
 }
 
+// exact arithmetic of the refine, the exact fallback and the k > FX_BIG_K path
+template <int DT>
+__device__ __forceinline__ void load_chunk(const char* p, float* v) {  // 16 bytes -> E floats
+    if (DT == F32) {
+        float4 x = *(const float4*)p;
+        v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+    } else {
+        uint4 x = *(const uint4*)p;
+        const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const uint16_t lo = (uint16_t)(w[e] & 0xffffu), hi = (uint16_t)(w[e] >> 16);
+            v[2 * e] = DT == BF16 ? bf2f(lo) : h2f(lo);
+            v[2 * e + 1] = DT == BF16 ? bf2f(hi) : h2f(hi);
+        }
+    }
+}
+
+// exact metric value of (x, row) accumulated by `nl` lanes (lane sub of nl)
+template <int DT, int METRIC>
+__device__ __forceinline__ double exact_partial(const float* __restrict__ xq, const char* __restrict__ yrow,
+                                                int row_bytes, int sub, int nl) {
+    constexpr int E = DT == F32 ? 4 : 8;
+    double acc = 0.0;
+    for (int c = sub; c * 16 < row_bytes; c += nl) {
+        float y[E];
+        load_chunk<DT>(yrow + c * 16, y);
+        const float* xc = xq + c * E;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            if (METRIC == L2) {
+                const double df = (double)xc[e] - (double)y[e];
+                acc = fma(df, df, acc);
+            } else {
+                acc = fma((double)xc[e], (double)y[e], acc);
+            }
+        }
+    }
+    return acc;
+}
+
 // ---------------------------------------------------------------------------
 // wave-level (64-lane) bitonic helpers on (key, id) pairs, ascending,
 // ties -> smaller id.  Used for LDS list compaction and every merge.

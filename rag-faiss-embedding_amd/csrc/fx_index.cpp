@@ -94,6 +94,7 @@ struct Options {
     int prune_rank = 0;      // FX_PRUNE_RANK: rank of the shared threshold (0: max(2k, 16))
     int compact_at = 0;      // FX_COMPACT_AT: list fill that triggers a compaction (0: default, KP < v <= CAP)
     int union_w = 0;         // FX_UNION_W: splits per union-bound window (16, 32, 64; 0: by split count)
+    int seed_tiles = 0;      // FX_SEED_TILES: threshold-seeding scan of the first tiles (-1 off, 0 auto, > 0 tiles)
     int scan_dbg = 0;        // FX_SCAN_DBG: ablation switches of -DFX_ABLATION builds / key dump (32)
     int graph_verbose = 0;   // FX_SEARCH_GRAPH_VERBOSE
     std::string trace, stamps, cand, keys;  // FX_SCAN_TRACE / _STAMPS / _CAND / _KEYS dump paths
@@ -116,6 +117,7 @@ struct Options {
         num("FX_PRUNE_RANK", prune_rank);
         num("FX_COMPACT_AT", compact_at);
         num("FX_UNION_W", union_w);
+        num("FX_SEED_TILES", seed_tiles);
         num("FX_SCAN_DBG", scan_dbg);
         num("FX_SEARCH_GRAPH_VERBOSE", graph_verbose);
         str("FX_SCAN_TRACE", trace);
@@ -125,9 +127,10 @@ struct Options {
     }
     int* find(const char* name) {
         static const char* names[] = {"search_graph", "force_fallback", "scan_place", "scan_sx", "reduce_cand",
-                                      "f32_split", "centre", "scan_pub", "prune_rank", "scan_dbg", "compact_at", "union_w"};
+                                      "f32_split", "centre", "scan_pub", "prune_rank", "scan_dbg", "compact_at", "union_w",
+                                      "seed_tiles"};
         int* slots[] = {&search_graph, &force_fallback, &place, &sx, &reduce_cand,
-                        &f32_split, &centre, &pub, &prune_rank, &scan_dbg, &compact_at, &union_w};
+                        &f32_split, &centre, &pub, &prune_rank, &scan_dbg, &compact_at, &union_w, &seed_tiles};
         for (int i = 0; i < (int)(sizeof(names) / sizeof(names[0])); ++i)
             if (strcmp(name, names[i]) == 0) return slots[i];
         return nullptr;
@@ -162,6 +165,8 @@ struct FxIndex {
     // the re-scan of uncertified queries (plan_rescan): its own query
     // operands, thresholds, candidate lists and flagged list
     DevBuf rq_f32, rq_op, rq_eps, rq_rho, rq_shift, rq_gtau, rq_cand_d, rq_cand_i, rq_flag;
+    // k > FX_BIG_K (fx_hugek.hip): query batch, sort keys, rocPRIM temporaries
+    DevBuf hk_ws;
     // scan image (ImageKind; rows [0, img_rows) current).  L2 images are
     // centred (Options.centre): mu = mean of a row sample, recomputed (and the
     // image rebuilt) whenever ntotal has doubled since (mu_rows), so the
@@ -397,6 +402,8 @@ struct SearchPlan {
     RefineParams rp{};
     PrepParams pp{};
     bool reduce = false;
+    ScanParams sps{};   // threshold-seeding scan (plan_seed), when `seed`
+    bool seed = false;
     size_t ncand = 0;
     // the re-scan of the queries pass 1 left uncertified (plan_rescan)
     ScanParams sp2{};
@@ -473,6 +480,41 @@ hipError_t plan_rescan(FxIndex* h, SearchPlan& P) {
     return hipSuccess;
 }
 
+// Cold-start thresholds (k <= KP): before the main scan, the same scan over
+// the corpus's first S tiles, without published lists, seeds the shared
+// per-query thresholds.  Every row it sees is a row of the corpus, so the
+// rank-th key of any of its splits bounds the query's global rank-th key from
+// above: the main scan starts pruning with it instead of +inf.  The main
+// scan's certification argument is unchanged (thresholds only fall; every
+// row a split drops lies above the final shared threshold).  Its candidate
+// lists land in the main scan's buffer (fewer splits), which the main scan
+// then overwrites.  Automatic only where the main scan's blocks walk few
+// tiles (cold lists are a visible share of their work).
+void plan_seed(const FxIndex* h, SearchPlan& P) {
+    const ScanParams& sp = P.sp;
+    P.seed = false;
+    const int opt = h->opt.seed_tiles;
+    if (!sp.share || opt < 0 || sp.dbg != 0) return;
+    const int per_block = sp.n_ctiles / std::max(1, sp.splits);
+    const int S = opt > 0 ? std::min(opt, sp.n_ctiles / 8) : std::min(256, sp.n_ctiles / 128);
+    if (S < 8 || (opt == 0 && per_block > 2048)) return;
+    ScanParams& ss = P.sps;
+    ss = sp;
+    ss.n_ctiles = S;
+    ss.ntotal = std::min<int64_t>(h->ntotal, (int64_t)S * TILE_R);
+    ss.place = 0;
+    ss.qt_per_xcd = 0;
+    ss.sx = 0;
+    ss.splits = std::min(sp.splits, std::max(1, std::min(S / 4, std::max(1, 256 / sp.n_qtiles))));
+    ss.grid = sp.n_qtiles * ss.splits;
+    ss.pub = nullptr;
+    ss.trace = nullptr;
+    ss.stamps = nullptr;
+    ss.dbgbuf = nullptr;
+    ss.seed_pass = 1;
+    P.seed = true;
+}
+
 hipError_t plan_search(FxIndex* h, int64_t nq, const void* qdev, int q_dtype, int k, float* Dd, int64_t* Id,
                        SearchPlan& P) {
     hipError_t e;
@@ -539,6 +581,8 @@ hipError_t plan_search(FxIndex* h, int64_t nq, const void* qdev, int q_dtype, in
     sp.dbgbuf = nullptr;
     sp.stamps = nullptr;
     sp.nq_dev = nullptr;
+    sp.seed_pass = 0;
+    plan_seed(h, P);
 
     if ((e = h->flag.ensure((size_t)(nq + 1) * 4)) != hipSuccess) return e;
     RefineParams& rp = P.rp;
@@ -591,6 +635,7 @@ hipError_t enqueue_search(FxIndex* h, SearchPlan& P, hipStream_t s, bool timed, 
         const size_t npub = (size_t)P.sp.n_qtiles * TILE_Q * P.sp.splits * KP;
         if ((e = hipMemsetD32Async((hipDeviceptr_t)P.sp.pub, 0x7f800000u, npub, s)) != hipSuccess) return e;  // +inf
     }
+    if (P.seed && (e = launch_scan(P.scan_dt, h->metric, P.sps, s)) != hipSuccess) return e;
     if (timed && (e = hipEventRecord(ev[0], s)) != hipSuccess) return e;
     if ((e = launch_scan(P.scan_dt, h->metric, P.sp, s)) != hipSuccess) return e;
     if (timed && (e = hipEventRecord(ev[1], s)) != hipSuccess) return e;
@@ -723,6 +768,56 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
     return FX_OK;
 }
 
+// k > FX_BIG_K: exact keys of every (query, row) pair and a radix sort per
+// query (fx_hugek.hip).  Every result is exact, so no query is "uncertified".
+int do_search_hugek(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int k, float* D, int64_t* I,
+                    int out_mem) {
+    hipStream_t s = h->stream();
+    const void* qdev = q;
+    if (q_mem == FX_MEM_HOST) {
+        HIP_TRY(h->qin.ensure((size_t)nq * h->d * dtype_size(q_dtype)));
+        HIP_TRY(hipMemcpyAsync(h->qin.p, q, (size_t)nq * h->d * dtype_size(q_dtype), hipMemcpyHostToDevice, s));
+        qdev = h->qin.p;
+    }
+    float* Dd = D;
+    int64_t* Id = I;
+    if (out_mem == FX_MEM_HOST) {
+        HIP_TRY(h->dws.ensure((size_t)nq * k * 4));
+        HIP_TRY(h->iws.ensure((size_t)nq * k * 8));
+        Dd = (float*)h->dws.p;
+        Id = (int64_t*)h->iws.p;
+    }
+    const int qb = hugek_batch(h->ntotal, nq);
+    size_t ws = 0;
+    HIP_TRY(hugek_workspace(h->ntotal, h->kdim, qb, &ws));
+    HIP_TRY(h->hk_ws.ensure(ws));
+    HugeKParams p{};
+    p.codes = h->codes;
+    p.row_bytes = h->row_bytes;
+    p.kdim = h->kdim;
+    p.d = h->d;
+    p.st_dt = h->dtype;
+    p.metric = h->metric;
+    p.ntotal = h->ntotal;
+    p.q = qdev;
+    p.q_dt = q_dtype;
+    p.nq = nq;
+    p.k = k;
+    p.id_offset = h->id_offset;
+    p.D = Dd;
+    p.I = Id;
+    HIP_TRY(launch_hugek_search(p, h->hk_ws.p, h->hk_ws.bytes, qb, s));
+    h->last_fallbacks = 0;
+    h->last_exact = 0;
+    h->fb_pending = false;
+    if (out_mem == FX_MEM_HOST) {
+        HIP_TRY(hipMemcpyAsync(D, Dd, (size_t)nq * k * 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(I, Id, (size_t)nq * k * 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    return FX_OK;
+}
+
 // Shape + options + every device buffer a captured search touches: the graph
 // is valid while all of them are unchanged
 std::vector<uint64_t> graph_key(const FxIndex* h, int64_t nq, int q_dtype, int k) {
@@ -730,8 +825,8 @@ std::vector<uint64_t> graph_key(const FxIndex* h, int64_t nq, int q_dtype, int k
     return {(uint64_t)nq, (uint64_t)q_dtype, (uint64_t)k, (uint64_t)h->ntotal, (uint64_t)h->id_offset,
             (uint64_t)h->img_kind, (uint64_t)h->centred, (uint64_t)h->img_rows,
             (uint64_t)o.force_fallback, (uint64_t)o.place, (uint64_t)o.sx, (uint64_t)o.reduce_cand,
-            (uint64_t)o.pub, (uint64_t)o.prune_rank,
-            (uint64_t)(uintptr_t)h->codes, (uint64_t)(uintptr_t)h->norms, (uint64_t)(uintptr_t)h->split.p,
+            (uint64_t)o.pub, (uint64_t)o.prune_rank, (uint64_t)o.compact_at, (uint64_t)o.union_w,
+            (uint64_t)o.seed_tiles, (uint64_t)(uintptr_t)h->codes, (uint64_t)(uintptr_t)h->norms, (uint64_t)(uintptr_t)h->split.p,
             (uint64_t)(uintptr_t)h->cnorms.p, (uint64_t)(uintptr_t)h->centre.p, (uint64_t)(uintptr_t)h->qshift.p,
             (uint64_t)(uintptr_t)h->qin.p, (uint64_t)(uintptr_t)h->qf32.p, (uint64_t)(uintptr_t)h->qop.p,
             (uint64_t)(uintptr_t)h->qeps.p, (uint64_t)(uintptr_t)h->qrho.p, (uint64_t)(uintptr_t)h->gtau.p,
@@ -902,7 +997,7 @@ void fx_index_free(FxIndex* h) {
                           &h->fbc_d, &h->fbc_i, &h->stage, &h->gtau, &h->trace, &h->dbgbuf, &h->split, &h->cnorms,
                           &h->centre, &h->mu_part, &h->qshift, &h->qrho, &h->stamps, &h->pub, &h->cand2_d,
                           &h->cand2_i, &h->rq_f32, &h->rq_op, &h->rq_eps, &h->rq_rho, &h->rq_shift, &h->rq_gtau,
-                          &h->rq_cand_d, &h->rq_cand_i, &h->rq_flag})
+                          &h->rq_cand_d, &h->rq_cand_i, &h->rq_flag, &h->hk_ws})
             b->release();
         graph_release(h);
         if (h->ghq) (void)hipHostFree(h->ghq);
@@ -1024,13 +1119,13 @@ int fx_index_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_me
     if (!h) return set_err(FX_E_ARG, "null index");
     if (nq < 0) return set_err(FX_E_ARG, "negative nq");
     if (k <= 0) return set_err(FX_E_ARG, "k must be positive (got %d)", k);
-    if (k > FX_MAX_K) return set_err(FX_E_UNSUPPORTED, "k=%d exceeds FX_MAX_K=%d", k, FX_MAX_K);
-    static_assert(FX_MAX_K == FX_BIG_K, "ABI k limit = the big-k refine's");
+    static_assert(FX_MAX_K == FX_BIG_K, "ABI k limit of the scan path = the big-k refine's");
     if (!check_dtype(q_dtype)) return set_err(FX_E_ARG, "bad query dtype %d", q_dtype);
     if (nq == 0) return FX_OK;
     if (!q || !D || !I) return set_err(FX_E_ARG, "null buffer");
     std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard g(h->device);
+    if (h->ntotal > 0 && k > FX_MAX_K) return do_search_hugek(h, nq, q, q_dtype, q_mem, k, D, I, out_mem);
     if (h->ntotal == 0) {
         // faiss: empty index -> every slot missing (I = -1, D = FLT_MAX)
         const float dfill = h->metric == L2 ? FLT_MAX : -FLT_MAX;
@@ -1201,12 +1296,15 @@ int fx_index_read(const char* path, int storage_dtype, int device, FxIndex** out
 
 int fx_merge_shards(int metric, int nshards, int64_t nq, int k, const float* D_in, const int64_t* I_in, float* D_out,
                     int64_t* I_out, int device, void* stream) {
-    if (nshards <= 0 || nq < 0 || k <= 0 || k > FX_MAX_K) return set_err(FX_E_ARG, "bad merge shape");
+    if (nshards <= 0 || nq < 0 || k <= 0) return set_err(FX_E_ARG, "bad merge shape");
     if (!D_in || !I_in || !D_out || !I_out) return set_err(FX_E_ARG, "null buffer");
     if (metric != FX_METRIC_L2 && metric != FX_METRIC_INNER_PRODUCT) return set_err(FX_E_ARG, "bad metric");
     DeviceGuard g(device);
     if (!g.ok) return set_err(FX_E_HIP, "hipSetDevice(%d) failed", device);
-    HIP_TRY(launch_merge_shards(metric, nshards, nq, k, D_in, I_in, D_out, I_out, (hipStream_t)stream));
+    if (k > FX_MAX_K)  // stream-ordered sort merge (fx_hugek.hip)
+        HIP_TRY(launch_merge_shards_sort(metric, nshards, nq, k, D_in, I_in, D_out, I_out, (hipStream_t)stream));
+    else
+        HIP_TRY(launch_merge_shards(metric, nshards, nq, k, D_in, I_in, D_out, I_out, (hipStream_t)stream));
     return FX_OK;
 }
 

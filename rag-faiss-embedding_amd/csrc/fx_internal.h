@@ -11,7 +11,8 @@ constexpr int TILE_R = 128;   // corpus rows per tile (MFMA M side)
 constexpr int TILE_Q = 128;   // queries per tile      (MFMA N side)
 constexpr int STAGE_B = 128;  // bytes of each row's K staged per pipeline stage
 constexpr int KP = 32;        // candidates kept per (query, corpus split)
-constexpr int FX_BIG_K = 1024;  // largest k (k > KP: k_refine_big; == FX_MAX_K of the ABI)
+constexpr int FX_BIG_K = 1024;  // largest k of the scan path (k > KP: k_refine_big; == FX_MAX_K of the
+                                // ABI); larger k: fx_hugek.hip
 constexpr int CAP = 64;       // LDS candidate-list capacity per query (2*KP)
 constexpr int ROW_ALIGN = 128;  // row stride alignment in bytes (== STAGE_B)
 constexpr int SCAN_THREADS = 256;
@@ -72,6 +73,8 @@ struct ScanParams {
                                 // [grid][4 waves][16] per-wave cycle sums of the scan's phases
     const int* nq_dev;          // non-null (the re-scan of uncertified queries): the live query
                                 // count is min(*nq_dev, nq), known only on the device
+    int seed_pass;              // 1: the threshold-seeding scan of the corpus's first tiles (its own
+                                // kernel instance, so profiles keep it apart from the main scan)
 };
 
 // queries are zero-padded to a multiple of QPAD (the scan's query tile)
@@ -164,6 +167,28 @@ hipError_t launch_exact_fallback(int st_dt, int metric, const char* codes, int r
                                  hipStream_t s);
 hipError_t launch_merge_shards(int metric, int nshards, int64_t nq, int k, const float* D_in,
                                const int64_t* I_in, float* D_out, int64_t* I_out, hipStream_t s);
+// k > FX_BIG_K (fx_hugek.hip): exact key of every (query, row) pair, a radix
+// sort per query, the first k -> D / I (faiss padding past ntotal)
+struct HugeKParams {
+    const char* codes;     // [ntotal][row_bytes] stored rows (storage dtype st_dt)
+    int row_bytes, kdim, d, st_dt, metric;
+    int64_t ntotal;
+    const void* q;         // [nq][d] queries on the device, dtype q_dt
+    int q_dt;
+    int64_t nq;
+    int k;
+    int64_t id_offset;
+    float* D;              // [nq][k] on the device
+    int64_t* I;
+};
+// queries per batch, and the workspace bytes a batch of qb queries needs
+int hugek_batch(int64_t ntotal, int64_t nq);
+hipError_t hugek_workspace(int64_t ntotal, int kdim, int qb, size_t* bytes);
+hipError_t launch_hugek_search(const HugeKParams& p, void* ws, size_t ws_bytes, int qb, hipStream_t s);
+// fx_merge_shards for k > FX_BIG_K: per query, a sort of the G*k entries by id
+// and then stably by distance (stream-ordered workspace)
+hipError_t launch_merge_shards_sort(int metric, int nshards, int64_t nq, int k, const float* D_in,
+                                    const int64_t* I_in, float* D_out, int64_t* I_out, hipStream_t s);
 // fp32 code rows [r0, r1) -> their F32S scan image (same row stride)
 // (centred by mu when non-null), with the image rows' |v|^2 -> cnorms and their
 // maximum -> cmax_bits (atomicMax)

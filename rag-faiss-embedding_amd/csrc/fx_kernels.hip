@@ -755,46 +755,6 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_topk(ScanParams p) {
 // ---------------------------------------------------------------------------
 // merge + exact refine + certification: one wave per query
 // ---------------------------------------------------------------------------
-template <int DT>
-__device__ __forceinline__ void load_chunk(const char* p, float* v) {  // 16 bytes -> E floats
-    if (DT == F32) {
-        float4 x = *(const float4*)p;
-        v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
-    } else {
-        uint4 x = *(const uint4*)p;
-        const uint32_t w[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const uint16_t lo = (uint16_t)(w[e] & 0xffffu), hi = (uint16_t)(w[e] >> 16);
-            v[2 * e] = DT == BF16 ? bf2f(lo) : h2f(lo);
-            v[2 * e + 1] = DT == BF16 ? bf2f(hi) : h2f(hi);
-        }
-    }
-}
-
-// exact metric value of (x, row) accumulated by `nl` lanes (lane sub of nl)
-template <int DT, int METRIC>
-__device__ __forceinline__ double exact_partial(const float* __restrict__ xq, const char* __restrict__ yrow,
-                                                int row_bytes, int sub, int nl) {
-    constexpr int E = DT == F32 ? 4 : 8;
-    double acc = 0.0;
-    for (int c = sub; c * 16 < row_bytes; c += nl) {
-        float y[E];
-        load_chunk<DT>(yrow + c * 16, y);
-        const float* xc = xq + c * E;
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-            if (METRIC == L2) {
-                const double df = (double)xc[e] - (double)y[e];
-                acc = fma(df, df, acc);
-            } else {
-                acc = fma((double)xc[e], (double)y[e], acc);
-            }
-        }
-    }
-    return acc;
-}
-
 // merge one chunk of 64 candidates (one per lane) into the running best-64
 __device__ __forceinline__ void refine_take(float d, int i, float& bd, int& bi, float& td, int& ti, int& nvalid,
                                             int lane) {

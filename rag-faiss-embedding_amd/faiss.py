@@ -118,17 +118,12 @@ class _FlatIndex:
 
     def search(self, x, k: int, *, D=None, I=None) -> Tuple:
         """``IndexFlat.search`` (faiss_store.py:64): k nearest rows of every
-        query row.  Returns ``(D, I)`` shaped ``(nq, k)``."""
+        query row.  Returns ``(D, I)`` shaped ``(nq, k)``.  Any k, as faiss:
+        k <= ``MAX_K`` runs the fused scan, larger k the exact sort path;
+        slots past ntotal hold I = -1, D = +-FLT_MAX."""
         k = int(k)
         if k <= 0:
             raise AssertionError("k must be positive")
-        if k > _lib.MAX_K:
-            # faiss pads with I = -1 / D = +-FLT_MAX beyond ntotal: serve k > MAX_K
-            # when the index holds at most MAX_K rows.
-            n = self.ntotal
-            if n > _lib.MAX_K:
-                raise RuntimeError(f"k={k} > {_lib.MAX_K} is not supported for an index of {n} rows")
-            return self._search_padded(x, k, max(n, 1))
         if _is_device_tensor(x):
             t = _torch()
             assert x.dim() == 2 and x.shape[1] == self.d, "dimension mismatch"
@@ -164,21 +159,6 @@ class _FlatIndex:
                                   Dh.ctypes.data_as(ctypes.c_void_p), Ih.ctypes.data_as(ctypes.c_void_p),
                                   _lib.MEM_HOST))
         return Dh, Ih
-
-    def _search_padded(self, x, k: int, k_eff: int):
-        D, I = self.search(x, k_eff)
-        fill = np.float32(3.4028234663852886e38) if self.metric_type == METRIC_L2 else np.float32(-3.4028234663852886e38)
-        if isinstance(D, np.ndarray):
-            Dp = np.full((D.shape[0], k), fill, dtype=np.float32)
-            Ip = np.full((D.shape[0], k), -1, dtype=np.int64)
-        else:
-            t = _torch()
-            Dp = t.full((D.shape[0], k), float(fill), dtype=t.float32, device=D.device)
-            Ip = t.full((D.shape[0], k), -1, dtype=t.int64, device=D.device)
-        if self.ntotal > 0:
-            Dp[:, :k_eff] = D
-            Ip[:, :k_eff] = I
-        return Dp, Ip
 
     def last_fallbacks(self) -> int:
         """Queries of the last search whose top-k the scan's candidates could

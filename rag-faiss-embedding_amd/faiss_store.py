@@ -67,12 +67,8 @@ class FAISSVectorStore:
     def search(self, query_vector, k: int = 5) -> Tuple[np.ndarray, List[int]]:
         """faiss_store.py:49-81: one query; index rows map to document ids,
         -1 and rows past the id list are dropped; on any error the result is
-        ``(np.array([]), [])``.
-
-        Known deviation: k is capped at ``FX_MAX_K`` = 1024 once the index
-        holds more than 1024 rows (faiss has no cap; the reference passes
-        k = 5).  A larger k then fails inside the index, and this method
-        swallows it like any other error, returning ``(np.array([]), [])``."""
+        ``(np.array([]), [])``.  Any k, as faiss (k > ``FX_MAX_K`` = 1024
+        takes the index's exact sort path)."""
         try:
             q = query_vector
             if isinstance(q, list):

@@ -5,7 +5,7 @@
 // usual: GPU sanitizers are not available on this pool), and run on the GPU
 // box by tests/test_native_asan.py.  It walks every entry point through the
 // paths that size host / device buffers by hand: growth by repeated adds,
-// k <= 32 and k > 32 searches, host and device result buffers, the
+// k <= 32, k > 32 and k > FX_MAX_K searches, host and device result buffers, the
 // graph-replayed small search, IxF2 write / read (fp32 and bf16 storage)
 // including truncated and foreign files, reset, and the argument-error paths.
 // Search results are checked against a float64 brute force on the host; any
@@ -98,8 +98,6 @@ int main() {
         int64_t I[5];
         float q[d] = {0};
         CHECK(fx_index_search(ix, 1, q, FX_F32, FX_MEM_HOST, 0, D, I, FX_MEM_HOST) != FX_OK, "k = 0 accepted");
-        CHECK(fx_index_search(ix, 1, q, FX_F32, FX_MEM_HOST, FX_MAX_K + 1, D, I, FX_MEM_HOST) != FX_OK,
-              "k > FX_MAX_K accepted");
         CHECK(fx_index_add(ix, 3, nullptr, FX_F32, FX_MEM_HOST) != FX_OK, "null rows accepted");
         // empty index: every slot is padding
         OK(fx_index_search(ix, 1, q, FX_F32, FX_MEM_HOST, 5, D, I, FX_MEM_HOST));
@@ -123,6 +121,9 @@ int main() {
     search_and_check(ix, xb, n, d, 77, 10, rng, "nq=77 k=10");
     search_and_check(ix, xb, n, d, 300, 32, rng, "nq=300 k=32");
     search_and_check(ix, xb, n, d, 9, 100, rng, "nq=9 k=100");
+    // k > FX_MAX_K: the exact sort path (fx_hugek.hip), also past ntotal (padding)
+    search_and_check(ix, xb, n, d, 5, FX_MAX_K + 500, rng, "nq=5 k=FX_MAX_K+500");
+    search_and_check(ix, xb, n, d, 3, (int)n + 40, rng, "nq=3 k=ntotal+40");
     int64_t fb = -1;
     OK(fx_index_last_fallbacks(ix, &fb));
     CHECK(fb >= 0, "fallback count");

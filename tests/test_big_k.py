@@ -7,7 +7,10 @@ Parity bar as in test_gpu_parity.py: ids bit-exact, |dD| <= 1e-5 max(1, |D|).
 k > 32 takes k_refine_big (block top-K re-rank of the splits' candidate
 lists, scan without the shared threshold); FX_FORCE_FALLBACK=1 flags every
 query so the device-gated exact fallback (k_fb_scan / k_fb_merge) produces
-every result.
+every result.  k > 1024 (FX_MAX_K) takes the exact sort path (fx_hugek.hip):
+exact keys of every (query, row) pair and one radix sort per query -- a
+segmented sort per batch up to 65,536 rows, a device-wide sort per query
+above -- so its results must equal the oracle's at any k.
 """
 import numpy as np
 import pytest
@@ -192,6 +195,83 @@ def test_merge_shards_big_k(fx, torch_cuda):
                              torch.tensor(np.stack(Is), device="cuda"), 150)
     Dr, Ir = C.knn_exact(xq, xb, 150)
     assert_parity(Dm.cpu().numpy(), Im.cpu().numpy(), Dr, Ir)
+
+
+@pytest.mark.parametrize("n", [20_000, 100_000])   # segmented sort / device-wide sort per query
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+def test_huge_k_parity(fx, n, dtype):
+    """k > FX_MAX_K: faiss takes any k (faiss_store.py:49,64)."""
+    rng = np.random.default_rng(41)
+    xb = rng.standard_normal((n, 96)).astype(np.float32)
+    xq = rng.standard_normal((20, 96)).astype(np.float32)
+    ix = fx.IndexFlatL2(96, dtype=dtype)
+    ix.add(xb)
+    for k in (1025, 3000):
+        D, I = ix.search(xq, k)
+        Dr, Ir = C.knn_exact(xq, ix.reconstruct_n(0, n), k)
+        assert_parity(D, I, Dr, Ir)
+        assert ix.last_fallbacks() == 0
+
+
+def test_huge_k_ties_and_padding(fx, torch_cuda):
+    """Duplicate rows (equal distances -> smaller id first), k past ntotal
+    (I = -1, D = FLT_MAX), device-resident queries and results, IP order."""
+    torch = torch_cuda
+    rng = np.random.default_rng(42)
+    base = rng.standard_normal((700, 48)).astype(np.float32)
+    xb = np.concatenate([base, base[::-1], base[:300]])          # 1700 rows, many exact ties
+    xq = np.concatenate([base[:4], rng.standard_normal((6, 48)).astype(np.float32)])
+    k = 2500
+    ix = fx.IndexFlatL2(48)
+    ix.add(xb)
+    D, I = ix.search(torch.tensor(xq, device="cuda"), k)
+    D, I = D.cpu().numpy(), I.cpu().numpy()
+    Dr, Ir = C.knn_exact(xq, xb, xb.shape[0])
+    assert_parity(D[:, :1700], I[:, :1700], Dr, Ir)
+    assert (I[:, 1700:] == -1).all() and (D[:, 1700:] == np.float32(3.4028234663852886e38)).all()
+    ip = fx.IndexFlatIP(48)
+    ip.add(xb)
+    D, I = ip.search(xq, 1200)
+    Dr, Ir = F.knn_inner_product(xq, xb, 1200)
+    assert_parity(D, I, Dr, Ir)
+
+
+def test_merge_shards_huge_k(fx, torch_cuda):
+    """fx_merge_shards with k > FX_MAX_K (sort by id, then stably by D)."""
+    torch = torch_cuda
+    rng = np.random.default_rng(43)
+    xb = rng.standard_normal((5000, 24)).astype(np.float32)
+    xb[4000:4400] = xb[100:500]                                   # ties across shards
+    xq = rng.standard_normal((12, 24)).astype(np.float32)
+    bounds = [0, 1100, 2300, 4100, 5000]
+    k = 1300
+    Ds, Is = [], []
+    for g in range(4):
+        ix = fx.IndexFlatL2(24)
+        ix.add(xb[bounds[g]:bounds[g + 1]])
+        ix.set_id_offset(bounds[g])
+        D, I = ix.search(xq, k)
+        Ds.append(D)
+        Is.append(I)
+    Dm, Im = fx.merge_shards(fx.METRIC_L2, torch.tensor(np.stack(Ds), device="cuda"),
+                             torch.tensor(np.stack(Is), device="cuda"), k)
+    Dr, Ir = C.knn_exact(xq, xb, k)
+    assert_parity(Dm.cpu().numpy(), Im.cpu().numpy(), Dr, Ir)
+
+
+def test_store_huge_k(fx):
+    """FAISSVectorStore.search with k > 1024 returns results (no silent ([], []))."""
+    from rag_faiss_embedding_amd.faiss_store import FAISSVectorStore
+    rng = np.random.default_rng(44)
+    xb = rng.standard_normal((3000, 32)).astype(np.float32)
+    FAISSVectorStore._instance = None
+    st = FAISSVectorStore(dimension=32)
+    st.add_vectors(xb, list(range(100, 3100)))
+    dist, ids = st.search(xb[7], k=2000)
+    Dr, Ir = C.knn_exact(xb[7:8], xb, 2000)
+    assert ids == [int(i) + 100 for i in Ir[0]]
+    assert np.allclose(dist, Dr[0], rtol=1e-5, atol=1e-5)
+    FAISSVectorStore._instance = None
 
 
 def test_output_buffer_checks(fx, torch_cuda):

@@ -17,9 +17,8 @@
 // the corpus is read once per batch of HK_QB queries (the key kernel keeps
 // HK_QB fp64 accumulators per row), the keys are written once and sorted.
 //
-// The shard merge (fx_merge_shards with k > FX_BIG_K) sorts each query's G*k
-// gathered entries twice -- by id, then stably by distance -- since global
-// ids need not fit the 32-bit field of the single-key form.
+// The shard merge (fx_merge_shards with k > FX_BIG_K) is a G-way merge of
+// each query's gathered lists (each already in the index order).
 #include "fx_device.h"
 
 #include <hipcub/hipcub.hpp>
@@ -240,97 +239,56 @@ hipError_t launch_hugek_search(const HugeKParams& p, void* ws, size_t ws_bytes, 
 }
 
 // ---------------------------------------------------------------------------
-// shard merge for k > FX_BIG_K
+// shard merge for k > FX_BIG_K: a G-way merge of each query's gathered lists
 // ---------------------------------------------------------------------------
-// entry (g, q0 + q, t) of the gathered [G][nq_all][k] lists -> position
-// q*G*k + g*k + t of the batch's query-major sort input: id key (missing:
-// last) and distance bits
-__global__ __launch_bounds__(HK_THREADS) void k_hkm_pack(int nshards, int64_t nq_all, int64_t q0, int64_t nq, int k,
-                                                         int metric,
-                                                         const float* __restrict__ D_in,
-                                                         const int64_t* __restrict__ I_in, uint64_t* __restrict__ idk,
-                                                         unsigned* __restrict__ dk) {
-    const int64_t per = (int64_t)nshards * k, total = nq * per;
-    for (int64_t i = (int64_t)blockIdx.x * HK_THREADS + threadIdx.x; i < total; i += (int64_t)gridDim.x * HK_THREADS) {
-        const int64_t q = i / per, r = i - q * per;
-        const int g = (int)(r / k), t = (int)(r - (int64_t)g * k);
-        const int64_t src = ((int64_t)g * nq_all + q0 + q) * k + t;
-        const int64_t id = I_in[src];
-        const float d = D_in[src];
-        idk[i] = id < 0 ? ~0ull : (uint64_t)id;
-        dk[i] = id < 0 ? 0xFFFFFFFFu : hk_ord(metric == L2 ? d : -d);
-    }
-}
+// Every per-shard list is already in the index order ((D, id) ascending for L2,
+// (-D, id) for IP; missing entries I = -1 last), so the merged top k is a
+// G-way merge: one thread per query keeps the G list heads and emits the
+// smallest k times (O(k G) per query; the rare large-k path).
+constexpr int HKM_MAXG = 64;
 
-__global__ __launch_bounds__(HK_THREADS) void k_hkm_out(int64_t per, int64_t nq, int k, int metric,
-                                                        const unsigned* __restrict__ dk,
-                                                        const uint64_t* __restrict__ idk, float* __restrict__ D,
-                                                        int64_t* __restrict__ I) {
-    const int64_t total = nq * k;
-    for (int64_t i = (int64_t)blockIdx.x * HK_THREADS + threadIdx.x; i < total; i += (int64_t)gridDim.x * HK_THREADS) {
-        const int64_t q = i / k, t = i - q * k;
-        const int64_t src = q * per + t;
-        const uint64_t id = t < per ? idk[src] : ~0ull;
-        if (id == ~0ull) {
-            D[i] = metric == L2 ? FLT_MAX : -FLT_MAX;
-            I[i] = -1;
-        } else {
-            const float f = ord2f(dk[src]);
-            D[i] = metric == L2 ? f : -f;
-            I[i] = (int64_t)id;
+__global__ __launch_bounds__(64) void k_hkm_merge(int nshards, int64_t nq, int k, int metric,
+                                                  const float* __restrict__ D_in, const int64_t* __restrict__ I_in,
+                                                  float* __restrict__ D_out, int64_t* __restrict__ I_out) {
+    const int64_t q = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    if (q >= nq) return;
+    int pos[HKM_MAXG];
+    float hk[HKM_MAXG];
+    int64_t hid[HKM_MAXG];
+    auto load = [&](int g) {
+        const int64_t src = ((int64_t)g * nq + q) * k + pos[g];
+        const int64_t id = pos[g] < k ? I_in[src] : -1;
+        hid[g] = id < 0 ? INT64_MAX : id;
+        hk[g] = id < 0 ? FX_INF : (metric == L2 ? D_in[src] : -D_in[src]);
+    };
+    for (int g = 0; g < nshards; ++g) {
+        pos[g] = 0;
+        load(g);
+    }
+    for (int t = 0; t < k; ++t) {
+        int best = 0;
+        for (int g = 1; g < nshards; ++g)
+            if (hk[g] < hk[best] || (hk[g] == hk[best] && hid[g] < hid[best])) best = g;
+        const int64_t o = q * k + t;
+        if (hid[best] == INT64_MAX) {
+            D_out[o] = metric == L2 ? FLT_MAX : -FLT_MAX;
+            I_out[o] = -1;
+            continue;
         }
+        D_out[o] = metric == L2 ? hk[best] : -hk[best];
+        I_out[o] = hid[best];
+        ++pos[best];
+        load(best);
     }
 }
 
 hipError_t launch_merge_shards_sort(int metric, int nshards, int64_t nq, int k, const float* D_in, const int64_t* I_in,
                                     float* D_out, int64_t* I_out, hipStream_t s) {
-    const int64_t per = (int64_t)nshards * k;
     if (nq <= 0) return hipSuccess;
-    if (per > INT_MAX) return hipErrorInvalidValue;
-    // queries per sort: <= 2^26 entries
-    const int64_t qb = std::max<int64_t>(1, std::min<int64_t>(nq, ((int64_t)1 << 26) / per));
-    const int64_t n = qb * per;
-    size_t t1 = 0, t2 = 0;
-    hipError_t e = hipcub::DeviceSegmentedRadixSort::SortPairs(
-        nullptr, t1, (const uint64_t*)nullptr, (uint64_t*)nullptr, (const unsigned*)nullptr, (unsigned*)nullptr,
-        (int)n, (int)qb, (const int*)nullptr, (const int*)nullptr, 0, 64, s);
-    if (e != hipSuccess) return e;
-    e = hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, t2, (const unsigned*)nullptr, (unsigned*)nullptr,
-                                                    (const uint64_t*)nullptr, (uint64_t*)nullptr, (int)n, (int)qb,
-                                                    (const int*)nullptr, (const int*)nullptr, 0, 32, s);
-    if (e != hipSuccess) return e;
-    const size_t tb = std::max(t1, t2);
-    const size_t o_idk2 = align_up((size_t)n * 8), o_dk = o_idk2 + align_up((size_t)n * 8),
-                 o_dk2 = o_dk + align_up((size_t)n * 4), o_offs = o_dk2 + align_up((size_t)n * 4),
-                 o_temp = o_offs + align_up((size_t)(qb + 1) * 4), total = o_temp + align_up(tb);
-    char* ws = nullptr;
-    if ((e = hipMallocAsync((void**)&ws, total, s)) != hipSuccess) return e;
-    uint64_t* idk = (uint64_t*)ws;
-    uint64_t* idk2 = (uint64_t*)(ws + o_idk2);
-    unsigned* dk = (unsigned*)(ws + o_dk);
-    unsigned* dk2 = (unsigned*)(ws + o_dk2);
-    int* offs = (int*)(ws + o_offs);
-    void* temp = ws + o_temp;
-    for (int64_t q0 = 0; q0 < nq && e == hipSuccess; q0 += qb) {
-        const int64_t nb = std::min<int64_t>(qb, nq - q0);
-        hipLaunchKernelGGL(k_hkm_pack, dim3(grid_for(nb * per)), dim3(HK_THREADS), 0, s, nshards, nq, q0, nb, k,
-                           metric, D_in, I_in, idk, dk);
-        hipLaunchKernelGGL(k_hk_offsets, dim3(1), dim3(256), 0, s, offs, (int)nb, (int)per);
-        size_t tt = tb;
-        // by id, then stably by distance: (D, id) order
-        e = hipcub::DeviceSegmentedRadixSort::SortPairs(temp, tt, idk, idk2, dk, dk2, (int)(nb * per), (int)nb, offs,
-                                                        offs + 1, 0, 64, s);
-        if (e != hipSuccess) break;
-        tt = tb;
-        e = hipcub::DeviceSegmentedRadixSort::SortPairs(temp, tt, dk2, dk, idk2, idk, (int)(nb * per), (int)nb, offs,
-                                                        offs + 1, 0, 32, s);
-        if (e != hipSuccess) break;
-        hipLaunchKernelGGL(k_hkm_out, dim3(grid_for(nb * k)), dim3(HK_THREADS), 0, s, per, nb, k, metric, dk, idk,
-                           D_out + q0 * k, I_out + q0 * k);
-        e = hipGetLastError();
-    }
-    const hipError_t ef = hipFreeAsync(ws, s);
-    return e != hipSuccess ? e : ef;
+    if (nshards > HKM_MAXG) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_hkm_merge, dim3((unsigned)((nq + 63) / 64)), dim3(64), 0, s, nshards, nq, k, metric, D_in,
+                       I_in, D_out, I_out);
+    return hipGetLastError();
 }
 
 }  // namespace fx

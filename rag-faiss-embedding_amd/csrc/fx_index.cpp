@@ -480,11 +480,13 @@ hipError_t plan_rescan(FxIndex* h, SearchPlan& P) {
     return hipSuccess;
 }
 
-// Cold-start thresholds (k <= KP): before the main scan, the same scan over
-// the corpus's first S tiles, without published lists, seeds the shared
-// per-query thresholds.  Every row it sees is a row of the corpus, so the
-// rank-th key of any of its splits bounds the query's global rank-th key from
-// above: the main scan starts pruning with it instead of +inf.  The main
+// Seeded thresholds (k <= KP): before the main scan, the same scan over the
+// corpus's first S tiles seeds the shared per-query thresholds.  Every row it
+// sees is a row of the corpus, so its union bound (the rank-th key of ~S*128
+// rows) bounds the query's global rank-th key from above: the main scan
+// starts pruning with it instead of +inf.  A streaming top-k sees about
+// k ln(N/k) rows beat its running threshold (each one a slow-path push);
+// started from the rank-th of S rows it sees about k (1 + ln(N/S)).  The main
 // scan's certification argument is unchanged (thresholds only fall; every
 // row a split drops lies above the final shared threshold).  Its candidate
 // lists land in the main scan's buffer (fewer splits), which the main scan
@@ -505,9 +507,12 @@ void plan_seed(const FxIndex* h, SearchPlan& P) {
     ss.place = 0;
     ss.qt_per_xcd = 0;
     ss.sx = 0;
-    ss.splits = std::min(sp.splits, std::max(1, std::min(S / 4, std::max(1, 256 / sp.n_qtiles))));
+    ss.splits = std::min(std::min(sp.splits, 64), std::max(1, std::min(S / 4, std::max(1, 256 / sp.n_qtiles))));
     ss.grid = sp.n_qtiles * ss.splits;
-    ss.pub = nullptr;
+    // its own published lists (in the main scan's pub buffer, cleared again
+    // before the main scan): the seeded threshold is the union bound over all
+    // of its splits, i.e. the rank-th key of about S * 128 rows
+    ss.union_w = ss.splits <= 16 ? 16 : ss.splits <= 32 ? 32 : 64;
     ss.trace = nullptr;
     ss.stamps = nullptr;
     ss.dbgbuf = nullptr;
@@ -635,8 +640,16 @@ hipError_t enqueue_search(FxIndex* h, SearchPlan& P, hipStream_t s, bool timed, 
         const size_t npub = (size_t)P.sp.n_qtiles * TILE_Q * P.sp.splits * KP;
         if ((e = hipMemsetD32Async((hipDeviceptr_t)P.sp.pub, 0x7f800000u, npub, s)) != hipSuccess) return e;  // +inf
     }
-    if (P.seed && (e = launch_scan(P.scan_dt, h->metric, P.sps, s)) != hipSuccess) return e;
+    // the timed scan window holds the seeding scan too (its launches show as
+    // their own kernel instance in a rocprof trace)
     if (timed && (e = hipEventRecord(ev[0], s)) != hipSuccess) return e;
+    if (P.seed) {
+        if ((e = launch_scan(P.scan_dt, h->metric, P.sps, s)) != hipSuccess) return e;
+        if (P.sp.pub) {  // the seeding scan's published lists are not the main scan's splits
+            const size_t npub = (size_t)P.sp.n_qtiles * TILE_Q * P.sp.splits * KP;
+            if ((e = hipMemsetD32Async((hipDeviceptr_t)P.sp.pub, 0x7f800000u, npub, s)) != hipSuccess) return e;
+        }
+    }
     if ((e = launch_scan(P.scan_dt, h->metric, P.sp, s)) != hipSuccess) return e;
     if (timed && (e = hipEventRecord(ev[1], s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(P.rp.n_flag, 0, 4, s)) != hipSuccess) return e;

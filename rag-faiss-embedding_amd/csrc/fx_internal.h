@@ -185,8 +185,8 @@ struct HugeKParams {
 int hugek_batch(int64_t ntotal, int64_t nq);
 hipError_t hugek_workspace(int64_t ntotal, int kdim, int qb, size_t* bytes);
 hipError_t launch_hugek_search(const HugeKParams& p, void* ws, size_t ws_bytes, int qb, hipStream_t s);
-// fx_merge_shards for k > FX_BIG_K: per query, a sort of the G*k entries by id
-// and then stably by distance (stream-ordered workspace)
+// fx_merge_shards for k > FX_BIG_K: per query, a G-way merge of the gathered
+// lists (each in the index order); at most 64 shards
 hipError_t launch_merge_shards_sort(int metric, int nshards, int64_t nq, int k, const float* D_in,
                                     const int64_t* I_in, float* D_out, int64_t* I_out, hipStream_t s);
 // fp32 code rows [r0, r1) -> their F32S scan image (same row stride)

@@ -94,7 +94,8 @@ struct Options {
     int prune_rank = 0;      // FX_PRUNE_RANK: rank of the shared threshold (0: max(2k, 16))
     int compact_at = 0;      // FX_COMPACT_AT: list fill that triggers a compaction (0: default, KP < v <= CAP)
     int union_w = 0;         // FX_UNION_W: splits per union-bound window (16, 32, 64; 0: by split count)
-    int seed_tiles = 0;      // FX_SEED_TILES: threshold-seeding scan of the first tiles (-1 off, 0 auto, > 0 tiles)
+    int seed_tiles = -1;     // FX_SEED_TILES: threshold-seeding scan of the first tiles (-1 off, 0 auto, > 0 tiles);
+                             // off by default: measured 2-5 % slower on (b), (d) nq=256 and the (d) shard
     int scan_dbg = 0;        // FX_SCAN_DBG: ablation switches of -DFX_ABLATION builds / key dump (32)
     int graph_verbose = 0;   // FX_SEARCH_GRAPH_VERBOSE
     std::string trace, stamps, cand, keys;  // FX_SCAN_TRACE / _STAMPS / _CAND / _KEYS dump paths
@@ -595,6 +596,7 @@ hipError_t plan_search(FxIndex* h, int64_t nq, const void* qdev, int q_dtype, in
     rp.cand_i = sp.cand_i;
     rp.splits = sp.splits;
     rp.nq = nq;
+    rp.ntotal = h->ntotal;
     rp.k = k;
     rp.codes = h->codes;
     rp.row_bytes = h->row_bytes;

@@ -107,6 +107,8 @@ struct RefineParams {
     const int* nq_dev;     // non-null: live query count min(*nq_dev, nq) (the re-scan)
     const int* out_idx;    // non-null: query q's results go to row out_idx[q] of D / I, and an
                            // uncertified q is flagged as out_idx[q] (the re-scan's gathered queries)
+    int64_t ntotal;        // rows of the index: a candidate row id outside [0, ntotal) is never gathered
+                           // (defence in depth: a list bug then shows as a parity failure, not a fault)
 };
 
 // exact fallback (k_fb_scan / k_fb_merge): corpus splits per flagged query,

@@ -872,7 +872,7 @@ __global__ __launch_bounds__(256) void k_refine(RefineParams p) {
                     const int64_t off = (((int64_t)qtile * p.splits + s) * TILE_Q + qq) * KP + j;
                     const float dd = p.cand_d[off];  // both loads in flight together
                     const int ii = p.cand_i[off];
-                    if (ii >= 0) { dv[u] = dd; iv[u] = ii; }
+                    if (ii >= 0 && ii < p.ntotal) { dv[u] = dd; iv[u] = ii; }
                 }
             }
 #pragma unroll
@@ -887,7 +887,7 @@ __global__ __launch_bounds__(256) void k_refine(RefineParams p) {
                 const int s = c / KP, j = c - s * KP;
                 const int64_t off = (((int64_t)qtile * p.splits + s) * TILE_Q + qq) * KP + j;
                 const int ii = p.cand_i[off];
-                if (ii >= 0) { d = p.cand_d[off]; i = ii; }
+                if (ii >= 0 && ii < p.ntotal) { d = p.cand_d[off]; i = ii; }
             }
             nvalid += __popcll(__ballot(i != INT_MAX));
             const bool pass = i != INT_MAX && key_lt(d, i, td, ti);
@@ -983,7 +983,7 @@ __global__ __launch_bounds__(BT_THREADS) void k_refine_big(RefineParams p) {
             const int s = c / KP, j = c - s * KP;
             const int64_t off = (((int64_t)qtile * p.splits + s) * TILE_Q + qq) * KP + j;
             const int ii = p.cand_i[off];
-            if (ii >= 0) {
+            if (ii >= 0 && ii < p.ntotal) {
                 d = p.cand_d[off];
                 i = ii;
                 valid = true;

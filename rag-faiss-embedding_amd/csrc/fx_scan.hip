@@ -48,18 +48,29 @@
 
 namespace fx {
 
-constexpr int S_NS = 5;                         // ring slots (S_NS - 1 stages in flight)
+// DMA ring slots (NS - 1 stages in flight): FX_V4_NS6 = 1 gives 6 where a
+// tile has >= 5 stages (needs LCAP <= 56 for the LDS), else 5.  Measured:
+// the deeper ring did not shorten the waits (they are barrier skew behind
+// slow-path tiles, not DMA latency) -- 5 slots is the default
+#ifndef FX_V4_NS6
+#define FX_V4_NS6 0
+#endif
+template <int KSTEPS>
+constexpr int ring_slots() { return (FX_V4_NS6 && KSTEPS / 2 >= 5) ? 6 : 5; }
 constexpr int S_STAGE = TILE_R * STAGE_B;       // 16 KiB = 128 rows x 128 B
 // norm / threshold slots first: every ring piece's LDS address is then >= 4 KiB,
 // more than any instruction offset subtracted from its M0 (see dma_piece)
 constexpr int S_NORM_OFF = 0;                   // 4 tile slots x 4 waves x 256 B
 constexpr int S_NSLOT_B = 4 * 256;              // [wave][32 row norms | 32 thresholds]
 constexpr int S_RING_OFF = S_NORM_OFF + 4 * S_NSLOT_B;
-constexpr int S_LD_OFF = S_RING_OFF + S_NS * S_STAGE;
-constexpr int S_LI_OFF = S_LD_OFF + TILE_Q * CAP * 4;
-constexpr int S_TRASH_OFF = S_LI_OFF + TILE_Q * CAP * 4;  // [4 waves][64 lanes] sink of the branch-free push
-constexpr int S_LDS_BYTES = S_TRASH_OFF + 4 * 256;
-static_assert(S_LDS_BYTES <= 160 * 1024, "LDS budget");
+template <int NS>
+struct ScanLds {
+    static constexpr int LD_OFF = S_RING_OFF + NS * S_STAGE;
+    static constexpr int LI_OFF = LD_OFF + TILE_Q * LCAP * 4;
+    static constexpr int TRASH_OFF = LI_OFF + TILE_Q * LCAP * 4;  // [4 waves][64 lanes] sink of the branch-free push
+    static constexpr int BYTES = TRASH_OFF + 4 * 256;
+    static_assert(BYTES <= 160 * 1024, "LDS budget");
+};
 
 // ABL: compile-time ablation switches of profiling builds (FX_ABLATION; 0 in
 // the product): 1 L2-resident corpus, 2 no corpus DMA, 4 no MFMA, 8 no
@@ -88,7 +99,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
     typedef typename AsmMmaV<DT>::A frag_t;
     typedef typename AsmMmaV<DT>::B bfrag_t;
     constexpr int SPT = KSTEPS / 2;  // stages per tile
-    constexpr int NS = S_NS;
+    constexpr int NS = ring_slots<KSTEPS>();
+    typedef ScanLds<NS> LDS;
     constexpr int M = TILE_R / 16;
     constexpr int N = 2;
     constexpr int RB = KSTEPS * 64;  // row stride in bytes
@@ -108,11 +120,11 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
     const int64_t q0 = (int64_t)qtile * TILE_Q;
     if (p.trace && tid == 0) trace_block_start(p, qtile, split);
 
-    float* lst_d = (float*)(smem + S_LD_OFF);
-    int* lst_i = (int*)(smem + S_LI_OFF);
+    float* lst_d = (float*)(smem + LDS::LD_OFF);
+    int* lst_i = (int*)(smem + LDS::LI_OFF);
     const int qw0 = wave * 32;  // this wave's queries (tile-local)
     const uint32_t ld_off = lds_off(lst_d), li_off = lds_off(lst_i);
-    const uint32_t trash = lds_off(smem + S_TRASH_OFF) + (uint32_t)(wave * 256 + lane * 4);
+    const uint32_t trash = lds_off(smem + LDS::TRASH_OFF) + (uint32_t)(wave * 256 + lane * 4);
     // list counts and thresholds of this lane's two queries (compact_regs)
     ListRegs lr;
     lr.cnt[0] = lr.cnt[1] = 0;
@@ -194,12 +206,13 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
     for (int n = 0; n < N; ++n) qloc[n] = qw0 + n * 16 + (lane & 15);
     const bool qv0 = q0 + qloc[0] < nq, qv1 = q0 + qloc[1] < nq;
     // per-lane LDS addresses: my two queries' list rows, my thresholds in a norm slot
-    const uint32_t lq[N] = {ld_off + (uint32_t)(qloc[0] * CAP * 4), ld_off + (uint32_t)(qloc[1] * CAP * 4)};
+    const uint32_t lq[N] = {ld_off + (uint32_t)(qloc[0] * LCAP * 4), ld_off + (uint32_t)(qloc[1] * LCAP * 4)};
     const uint32_t li_d = li_off - ld_off;
     const uint32_t gt_lane = (uint32_t)(128 + (lane & 15) * 4);
     const uint32_t nrm_lane = (uint32_t)(rl0 * 4);
 
-    asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");  // stage 0 (5 pieces) landed
+    // stage 0 (4 corpus pieces + the norm piece) landed: younger are stages 1 .. NS-2
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"(4 * (NS - 2)) : "memory");
     __builtin_amdgcn_sched_barrier(0);
     // fragment-read lane offset within a stage slot (half 0); half 1 is at
     // + rd_h1 (LN = 0: the next 1 KiB block; LN = 1: chunk + 4 under the
@@ -246,10 +259,12 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
             const int tnext = t + (nxt ? 1 : 0);
             // stage g+1 landed for every wave; X (half 0 of stage g) is in registers;
             // slot c4 is no longer read by anyone
-            // VMEM ops younger than stage g+1's: those issued in stages g-2, g-1
-            // (4 corpus pieces each, + the norm piece where that stage
-            // prefetched a tile's first stage)
-            constexpr int W = 8 + ((j + 3) % SPT == 0) + ((j + 2) % SPT == 0);
+            // VMEM ops younger than stage g+1's: stages g+2 .. g+NS-2, issued
+            // in the NS-3 stages before this one (4 corpus pieces each, + the
+            // norm piece with a tile's first stage)
+            constexpr int W = 4 * (NS - 3) + ((j + 2) % SPT == 0) + ((j + 3) % SPT == 0) +
+                              (NS >= 6 && (j + 4) % SPT == 0);
+            static_assert(NS == 5 || NS == 6, "wait count written for 5 or 6 slots");
             uint64_t s_a = 0, s_b = 0, s_c = 0;
             if constexpr (ABL & 64) {
                 s_a = __builtin_amdgcn_s_memtime();
@@ -442,12 +457,13 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
             });
             if constexpr (ABL & (64 | 1024)) stq[11] += __builtin_amdgcn_s_memtime() - s_sl;
             // compact every list that reached p.compact_at (and any that overflowed)
-            bool need = ovf || lr.cnt[0] >= p.compact_at || lr.cnt[1] >= p.compact_at;
+            const int cat = min(p.compact_at, LCAP);  // the plan's trigger, within this kernel's lists
+            bool need = ovf || lr.cnt[0] >= cat || lr.cnt[1] >= cat;
             while (__builtin_amdgcn_ballot_w64(need)) {
                 uint64_t s_cp = 0;
                 if constexpr (ABL & (64 | 1024)) s_cp = __builtin_amdgcn_s_memtime();
                 lr = compact_regs(lst_d, lst_i, lr, p.share ? gtq : nullptr, qw0, lane, p.pub ? pubw : nullptr, p.splits,
-                                  split, p.prune_rank, p.compact_at, p.union_w);
+                                  split, p.prune_rank, cat, p.union_w);
                 if constexpr (ABL & (64 | 1024)) {
                     stq[8] += 1;
                     stq[9] += __builtin_amdgcn_s_memtime() - s_cp;
@@ -497,9 +513,9 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
         const int q = qw0 + qi;
         if (q0 + q >= nq) break;
         const int cq = qi < 16 ? __builtin_amdgcn_readlane(lr.cnt[0], qi) : __builtin_amdgcn_readlane(lr.cnt[1], qi - 16);
-        const int cn = min(cq, CAP);
-        float d = lane < cn ? lst_d[q * CAP + lane] : FX_INF;
-        int i = lane < cn ? lst_i[q * CAP + lane] : INT_MAX;
+        const int cn = min(cq, LCAP);
+        float d = lane < cn ? lst_d[q * LCAP + lane] : FX_INF;
+        int i = lane < cn ? lst_i[q * LCAP + lane] : INT_MAX;
         sort64(d, i, lane);
         if (lane < KP) {
             p.cand_d[(obase + q) * KP + lane] = d;
@@ -542,11 +558,12 @@ static hipError_t scan_v4_t(const ScanParams& p, hipStream_t s) {
         }
     }
 #endif
+    constexpr int LDS_BYTES = ScanLds<ring_slots<KSTEPS>()>::BYTES;
     hipError_t e = g_graph_capture ? hipSuccess
                                    : hipFuncSetAttribute((const void*)k_scan_v4<DT, METRIC, KSTEPS, ABL, LN>,
-                                                         hipFuncAttributeMaxDynamicSharedMemorySize, S_LDS_BYTES);
+                                                         hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((k_scan_v4<DT, METRIC, KSTEPS, ABL, LN>), dim3(p.grid), dim3(SCAN_THREADS), S_LDS_BYTES, s, p);
+    hipLaunchKernelGGL((k_scan_v4<DT, METRIC, KSTEPS, ABL, LN>), dim3(p.grid), dim3(SCAN_THREADS), LDS_BYTES, s, p);
     return hipGetLastError();
 }
 

@@ -12,6 +12,15 @@ namespace fx {
 // Largest finite float: thresholds start here, so real keys always pass and
 // padding rows (|y|^2 = +inf -> key +inf) never do.
 constexpr float KEY_MAX = FLT_MAX;
+// k_scan_v4's per-query LDS list capacity (KP < LCAP <= 64, one sort64 lane
+// per entry).  56 leaves room for a 6-slot DMA ring (fx_scan.hip FX_V4_NS6);
+// that pair measured 1-2 % slower than 64 entries with 5 slots on (d), (b)
+// and (d) at nq = 256 (profiles/r3/ab/ns6_seed), so 64 is the default
+#ifndef FX_V4_LCAP
+#define FX_V4_LCAP 64
+#endif
+constexpr int LCAP = FX_V4_LCAP;
+static_assert(LCAP > KP && LCAP <= 64, "list capacity");
 // global-address-space float: loads through it are global_load (vmcnt only),
 // not flat (which also counts against lgkmcnt as a possible LDS access)
 typedef __attribute__((address_space(1))) float gfloat;
@@ -114,7 +123,7 @@ __device__ __forceinline__ void ds_wr32(uint32_t off, int v) {
 
 // Per-wave candidate lists of k_scan_v4.  The wave owns 32 queries: query
 // column c of accumulator half n (lanes with lane & 15 == c, n = 0, 1) is
-// tile-local query qw0 + 16 n + c.  Each list lives in LDS ([query][CAP] keys
+// tile-local query qw0 + 16 n + c.  Each list lives in LDS ([query][LCAP] keys
 // and rows); its entry count and its pruning threshold live in registers
 // (cntv[n], tauv[n]), the same value in the 4 lanes that hold the query, so a
 // push reserves its slots without an LDS atomic round trip.
@@ -151,7 +160,7 @@ __device__ __forceinline__ bool push_reg(const f32x4 (&acc)[M][N], int n, int m,
     for (int i = 0; i < 4; ++i) {
         const int slot = s + (int)__popc(msk & ((1u << i) - 1u));
         const bool take = (msk >> i) & 1u;
-        const bool ok = take && slot < CAP;
+        const bool ok = take && slot < LCAP;
         const uint32_t e = lq + (uint32_t)slot * 4u;
         ds_wr32(ok ? e : trash, acc[m][n][i]);
         ds_wr32(ok ? e + li_d : trash, row0 + i);
@@ -162,11 +171,11 @@ __device__ __forceinline__ bool push_reg(const f32x4 (&acc)[M][N], int n, int m,
     return late != 0u;
 }
 
-// Compact this wave's lists that hold `at` or more entries (KP < at <= CAP)
+// Compact this wave's lists that hold `at` or more entries (KP < at <= LCAP)
 // to their KP best; the list's threshold becomes its rank-th key (rank = KP
 // unless the union bound is on), published to the shared per-query threshold.
 // A list's threshold only improves here, so compacting before the list is
-// full (at < CAP) trades more compactions for fewer slow-path tiles.
+// full (at < LCAP) trades more compactions for fewer slow-path tiles.
 //
 // pub (k <= KP): the compacted list is also published to pub[query][split][KP],
 // and the shared threshold becomes the rank-th smallest key of the union of
@@ -201,13 +210,16 @@ __device__ __forceinline__ ListRegs compact_regs(float* lst_d, int* lst_i, ListR
         // entries past the count are stale (rows of earlier rounds: kept or
         // dropped ones, so possibly duplicates) unless the list is full
         const int cq = __builtin_amdgcn_readlane(qi < 16 ? cntv[0] : cntv[1], qi & 15);
-        const bool live = lane < cq;  // cq may exceed CAP (overflowed pushes wait in `pend`)
-        float d = live ? lst_d[q * CAP + lane] : FX_INF;
-        int i = live ? lst_i[q * CAP + lane] : INT_MAX;
+        // cq may exceed LCAP (overflowed pushes wait in `pend`): only the first
+        // LCAP lanes hold entries of this list (lanes past it would read the
+        // next query's row)
+        const bool live = lane < cq && lane < LCAP;
+        float d = live ? lst_d[q * LCAP + lane] : FX_INF;
+        int i = live ? lst_i[q * LCAP + lane] : INT_MAX;
         sort64(d, i, lane);
         if (lane < KP) {
-            lst_d[q * CAP + lane] = d;
-            lst_i[q * CAP + lane] = i;
+            lst_d[q * LCAP + lane] = d;
+            lst_i[q * LCAP + lane] = i;
         }
         const float dr = readlane_f(d, rank - 1);
         if ((lane & 15) == (qi & 15)) {

@@ -22,12 +22,14 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 SCAN = os.environ.get("FX_PROFILE_KERNEL", "k_scan_")  # k_scan_v4 / k_scan_q32
-RESCAN_MARK = (", 4096,", "Li4096E")  # fx_scan.hip RESCAN: the re-scan's own instance
+# fx_scan.hip RESCAN / SEED: the re-scan's and the threshold-seeding scan's own instances
+OTHER_MARKS = (", 4096,", "Li4096E", ", 8192,", "Li8192E")
 
 
 def is_scan(name):
-    """The main scan's launches, not the re-scan of uncertified queries."""
-    return SCAN in name and not any(m in name for m in RESCAN_MARK)
+    """The main scan's launches, not the re-scan of uncertified queries or the
+    threshold-seeding scan."""
+    return SCAN in name and not any(m in name for m in OTHER_MARKS)
 
 
 def counters(path):
@@ -51,13 +53,13 @@ def main():
         for r in csv.DictReader(f):
             kern[r["Name"]] = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6,
                                "pct": float(r["Percentage"])}
+    scan_name = next(n for n in kern if is_scan(n))
     pmc = {}
     for sub in ("fetch", "write", "tcc", "sq", "lds", "ta"):
         for name, cs in counters(prof / sub / "run_counter_collection.csv").items():
-            if is_scan(name):
+            if name == scan_name:
                 for c, vals in cs.items():
                     pmc[c] = statistics.median(vals)
-    scan_name = next(n for n in kern if is_scan(n))
     res = {"kernels": kern, "scan_kernel": scan_name, "scan_pmc_median_per_launch": pmc,
            "rows_per_gpu": rows, "nq": nq}
     if "FETCH_SIZE" in pmc:

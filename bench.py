@@ -396,8 +396,7 @@ def main():
     roof["traffic"] = None if variant else read_pmc_traffic(args.config, n_local, nq, args.data)
     roof["kernel"] = "k_scan_v4" + \
         (" F32S (fp32 as 3 bf16 MFMA products)" if split else "") + \
-        " (fused MFMA distance GEMM + top-k select; the timed window also holds the index's threshold-seeding" \
-        " launch of the same kernel where it runs one)"
+        " (fused MFMA distance GEMM + top-k select)"
     roof["kernel_ms_avg"] = round(scan_avg_ms, 4)
     roof["launches"] = launches
     roof["merge_refine_ms_avg"] = round(merge_ms / max(launches, 1), 4)

@@ -95,9 +95,8 @@ int fx_index_set_stream(FxIndex* index, void* stream);
  * (test hook: every query through the exact fallback), "scan_place",
  * "scan_sx", "reduce_cand", "f32_split", "centre", "scan_pub", "prune_rank",
  * "compact_at" (list fill that triggers a compaction), "union_w" (splits per
- * union-bound window), "seed_tiles" (threshold-seeding scan; -1 off), "pace_w"
- * (pacing window of a split's query-tile blocks; 0 off), "scan_dbg" (see
- * DESIGN.md 3).  Unknown name: FX_E_ARG. */
+ * union-bound window), "scan_dbg" (see DESIGN.md 3).  Unknown name:
+ * FX_E_ARG. */
 int fx_index_set_option(FxIndex* index, const char* name, int64_t value);
 /* Global id of local row 0 (row-sharded multi-GPU: shard offset). */
 int fx_index_set_id_offset(FxIndex* index, int64_t offset);

@@ -94,8 +94,6 @@ struct Options {
     int prune_rank = 0;      // FX_PRUNE_RANK: rank of the shared threshold (0: max(2k, 16))
     int compact_at = 0;      // FX_COMPACT_AT: list fill that triggers a compaction (0: default, KP < v <= CAP)
     int union_w = 0;         // FX_UNION_W: splits per union-bound window (16, 32, 64; 0: by split count)
-    int seed_tiles = -1;     // FX_SEED_TILES: threshold-seeding scan of the first tiles (-1 off, 0 auto, > 0 tiles);
-                             // off by default: measured 2-5 % slower on (b), (d) nq=256 and the (d) shard
     int scan_dbg = 0;        // FX_SCAN_DBG: ablation switches of -DFX_ABLATION builds / key dump (32)
     int graph_verbose = 0;   // FX_SEARCH_GRAPH_VERBOSE
     std::string trace, stamps, cand, keys;  // FX_SCAN_TRACE / _STAMPS / _CAND / _KEYS dump paths
@@ -118,7 +116,6 @@ struct Options {
         num("FX_PRUNE_RANK", prune_rank);
         num("FX_COMPACT_AT", compact_at);
         num("FX_UNION_W", union_w);
-        num("FX_SEED_TILES", seed_tiles);
         num("FX_SCAN_DBG", scan_dbg);
         num("FX_SEARCH_GRAPH_VERBOSE", graph_verbose);
         str("FX_SCAN_TRACE", trace);
@@ -128,10 +125,9 @@ struct Options {
     }
     int* find(const char* name) {
         static const char* names[] = {"search_graph", "force_fallback", "scan_place", "scan_sx", "reduce_cand",
-                                      "f32_split", "centre", "scan_pub", "prune_rank", "scan_dbg", "compact_at", "union_w",
-                                      "seed_tiles"};
+                                      "f32_split", "centre", "scan_pub", "prune_rank", "scan_dbg", "compact_at", "union_w"};
         int* slots[] = {&search_graph, &force_fallback, &place, &sx, &reduce_cand,
-                        &f32_split, &centre, &pub, &prune_rank, &scan_dbg, &compact_at, &union_w, &seed_tiles};
+                        &f32_split, &centre, &pub, &prune_rank, &scan_dbg, &compact_at, &union_w};
         for (int i = 0; i < (int)(sizeof(names) / sizeof(names[0])); ++i)
             if (strcmp(name, names[i]) == 0) return slots[i];
         return nullptr;
@@ -403,8 +399,6 @@ struct SearchPlan {
     RefineParams rp{};
     PrepParams pp{};
     bool reduce = false;
-    ScanParams sps{};   // threshold-seeding scan (plan_seed), when `seed`
-    bool seed = false;
     size_t ncand = 0;
     // the re-scan of the queries pass 1 left uncertified (plan_rescan)
     ScanParams sp2{};
@@ -481,46 +475,6 @@ hipError_t plan_rescan(FxIndex* h, SearchPlan& P) {
     return hipSuccess;
 }
 
-// Seeded thresholds (k <= KP): before the main scan, the same scan over the
-// corpus's first S tiles seeds the shared per-query thresholds.  Every row it
-// sees is a row of the corpus, so its union bound (the rank-th key of ~S*128
-// rows) bounds the query's global rank-th key from above: the main scan
-// starts pruning with it instead of +inf.  A streaming top-k sees about
-// k ln(N/k) rows beat its running threshold (each one a slow-path push);
-// started from the rank-th of S rows it sees about k (1 + ln(N/S)).  The main
-// scan's certification argument is unchanged (thresholds only fall; every
-// row a split drops lies above the final shared threshold).  Its candidate
-// lists land in the main scan's buffer (fewer splits), which the main scan
-// then overwrites.  Automatic only where the main scan's blocks walk few
-// tiles (cold lists are a visible share of their work).
-void plan_seed(const FxIndex* h, SearchPlan& P) {
-    const ScanParams& sp = P.sp;
-    P.seed = false;
-    const int opt = h->opt.seed_tiles;
-    if (!sp.share || opt < 0 || sp.dbg != 0) return;
-    const int per_block = sp.n_ctiles / std::max(1, sp.splits);
-    const int S = opt > 0 ? std::min(opt, sp.n_ctiles / 8) : std::min(256, sp.n_ctiles / 128);
-    if (S < 8 || (opt == 0 && per_block > 2048)) return;
-    ScanParams& ss = P.sps;
-    ss = sp;
-    ss.n_ctiles = S;
-    ss.ntotal = std::min<int64_t>(h->ntotal, (int64_t)S * TILE_R);
-    ss.place = 0;
-    ss.qt_per_xcd = 0;
-    ss.sx = 0;
-    ss.splits = std::min(std::min(sp.splits, 64), std::max(1, std::min(S / 4, std::max(1, 256 / sp.n_qtiles))));
-    ss.grid = sp.n_qtiles * ss.splits;
-    // its own published lists (in the main scan's pub buffer, cleared again
-    // before the main scan): the seeded threshold is the union bound over all
-    // of its splits, i.e. the rank-th key of about S * 128 rows
-    ss.union_w = ss.splits <= 16 ? 16 : ss.splits <= 32 ? 32 : 64;
-    ss.trace = nullptr;
-    ss.stamps = nullptr;
-    ss.dbgbuf = nullptr;
-    ss.seed_pass = 1;
-    P.seed = true;
-}
-
 hipError_t plan_search(FxIndex* h, int64_t nq, const void* qdev, int q_dtype, int k, float* Dd, int64_t* Id,
                        SearchPlan& P) {
     hipError_t e;
@@ -587,8 +541,6 @@ hipError_t plan_search(FxIndex* h, int64_t nq, const void* qdev, int q_dtype, in
     sp.dbgbuf = nullptr;
     sp.stamps = nullptr;
     sp.nq_dev = nullptr;
-    sp.seed_pass = 0;
-    plan_seed(h, P);
 
     if ((e = h->flag.ensure((size_t)(nq + 1) * 4)) != hipSuccess) return e;
     RefineParams& rp = P.rp;
@@ -642,16 +594,7 @@ hipError_t enqueue_search(FxIndex* h, SearchPlan& P, hipStream_t s, bool timed, 
         const size_t npub = (size_t)P.sp.n_qtiles * TILE_Q * P.sp.splits * KP;
         if ((e = hipMemsetD32Async((hipDeviceptr_t)P.sp.pub, 0x7f800000u, npub, s)) != hipSuccess) return e;  // +inf
     }
-    // the timed scan window holds the seeding scan too (its launches show as
-    // their own kernel instance in a rocprof trace)
     if (timed && (e = hipEventRecord(ev[0], s)) != hipSuccess) return e;
-    if (P.seed) {
-        if ((e = launch_scan(P.scan_dt, h->metric, P.sps, s)) != hipSuccess) return e;
-        if (P.sp.pub) {  // the seeding scan's published lists are not the main scan's splits
-            const size_t npub = (size_t)P.sp.n_qtiles * TILE_Q * P.sp.splits * KP;
-            if ((e = hipMemsetD32Async((hipDeviceptr_t)P.sp.pub, 0x7f800000u, npub, s)) != hipSuccess) return e;
-        }
-    }
     if ((e = launch_scan(P.scan_dt, h->metric, P.sp, s)) != hipSuccess) return e;
     if (timed && (e = hipEventRecord(ev[1], s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(P.rp.n_flag, 0, 4, s)) != hipSuccess) return e;
@@ -841,7 +784,7 @@ std::vector<uint64_t> graph_key(const FxIndex* h, int64_t nq, int q_dtype, int k
             (uint64_t)h->img_kind, (uint64_t)h->centred, (uint64_t)h->img_rows,
             (uint64_t)o.force_fallback, (uint64_t)o.place, (uint64_t)o.sx, (uint64_t)o.reduce_cand,
             (uint64_t)o.pub, (uint64_t)o.prune_rank, (uint64_t)o.compact_at, (uint64_t)o.union_w,
-            (uint64_t)o.seed_tiles, (uint64_t)(uintptr_t)h->codes, (uint64_t)(uintptr_t)h->norms, (uint64_t)(uintptr_t)h->split.p,
+            (uint64_t)(uintptr_t)h->codes, (uint64_t)(uintptr_t)h->norms, (uint64_t)(uintptr_t)h->split.p,
             (uint64_t)(uintptr_t)h->cnorms.p, (uint64_t)(uintptr_t)h->centre.p, (uint64_t)(uintptr_t)h->qshift.p,
             (uint64_t)(uintptr_t)h->qin.p, (uint64_t)(uintptr_t)h->qf32.p, (uint64_t)(uintptr_t)h->qop.p,
             (uint64_t)(uintptr_t)h->qeps.p, (uint64_t)(uintptr_t)h->qrho.p, (uint64_t)(uintptr_t)h->gtau.p,

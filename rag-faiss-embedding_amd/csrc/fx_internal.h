@@ -73,8 +73,6 @@ struct ScanParams {
                                 // [grid][4 waves][16] per-wave cycle sums of the scan's phases
     const int* nq_dev;          // non-null (the re-scan of uncertified queries): the live query
                                 // count is min(*nq_dev, nq), known only on the device
-    int seed_pass;              // 1: the threshold-seeding scan of the corpus's first tiles (its own
-                                // kernel instance, so profiles keep it apart from the main scan)
 };
 
 // queries are zero-padded to a multiple of QPAD (the scan's query tile)

@@ -91,7 +91,6 @@ struct ScanLds {
 //           address (LDS-DMA writes lane-linearly), and the fragment reads
 //           undo it, conflict-free for both K halves.
 constexpr int RESCAN = 4096;  // ABL bit naming the re-scan's instance (no code change)
-constexpr int SEED = 8192;    // ABL bit naming the threshold-seeding scan's instance (no code change)
 
 template <int DT, int METRIC, int KSTEPS, int ABL = 0, int LN = 0>
 __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
@@ -571,26 +570,13 @@ template <int DT, int METRIC>
 static hipError_t scan_rows(const ScanParams& p, hipStream_t s, bool* handled) {
     *handled = true;
     switch (p.row_bytes / 64) {
-        // the re-scan of uncertified queries (p.nq_dev set) and the
-        // threshold-seeding scan run the same code under their own kernel
-        // names (ABL bits RESCAN / SEED change nothing else), so profiles keep
-        // the main scan's launches apart from them
-        case 8:
-            return p.nq_dev      ? scan_v4_t<DT, METRIC, 8, RESCAN>(p, s)
-                   : p.seed_pass ? scan_v4_t<DT, METRIC, 8, SEED>(p, s)
-                                 : scan_v4_t<DT, METRIC, 8>(p, s);
-        case 12:
-            return p.nq_dev      ? scan_v4_t<DT, METRIC, 12, RESCAN>(p, s)
-                   : p.seed_pass ? scan_v4_t<DT, METRIC, 12, SEED>(p, s)
-                                 : scan_v4_t<DT, METRIC, 12>(p, s);
-        case 16:
-            return p.nq_dev      ? scan_v4_t<DT, METRIC, 16, RESCAN>(p, s)
-                   : p.seed_pass ? scan_v4_t<DT, METRIC, 16, SEED>(p, s)
-                                 : scan_v4_t<DT, METRIC, 16>(p, s);
-        case 24:
-            return p.nq_dev      ? scan_v4_t<DT, METRIC, 24, RESCAN>(p, s)
-                   : p.seed_pass ? scan_v4_t<DT, METRIC, 24, SEED>(p, s)
-                                 : scan_v4_t<DT, METRIC, 24>(p, s);
+        // the re-scan of uncertified queries (p.nq_dev set) runs the same code
+        // under its own kernel name (ABL bit RESCAN changes nothing else), so
+        // profiles keep the main scan's launches apart from it
+        case 8: return p.nq_dev ? scan_v4_t<DT, METRIC, 8, RESCAN>(p, s) : scan_v4_t<DT, METRIC, 8>(p, s);
+        case 12: return p.nq_dev ? scan_v4_t<DT, METRIC, 12, RESCAN>(p, s) : scan_v4_t<DT, METRIC, 12>(p, s);
+        case 16: return p.nq_dev ? scan_v4_t<DT, METRIC, 16, RESCAN>(p, s) : scan_v4_t<DT, METRIC, 16>(p, s);
+        case 24: return p.nq_dev ? scan_v4_t<DT, METRIC, 24, RESCAN>(p, s) : scan_v4_t<DT, METRIC, 24>(p, s);
         default: *handled = false; return hipSuccess;
     }
 }

@@ -91,7 +91,7 @@ struct Options {
     int f32_split = 1;       // FX_F32_SPLIT: fp32 indexes scan their split-bf16 image
     int centre = 1;          // FX_CENTER: L2 scan images are centred on a row sample's mean
     int pub = 1;             // FX_SCAN_PUB: union threshold over published per-split lists
-    int prune_rank = 0;      // FX_PRUNE_RANK: rank of the shared threshold (0: max(3k/2, 16))
+    int prune_rank = 0;      // FX_PRUNE_RANK: rank of the shared threshold (0: max(6k/5, 12))
     int compact_at = 0;      // FX_COMPACT_AT: list fill that triggers a compaction (0: default, KP < v <= CAP)
     int union_w = 0;         // FX_UNION_W: splits per union-bound window (16, 32, 64; 0: by split count)
     int scan_dbg = 0;        // FX_SCAN_DBG: ablation switches of -DFX_ABLATION builds / key dump (32)
@@ -527,11 +527,11 @@ hipError_t plan_search(FxIndex* h, int64_t nq, const void* qdev, int q_dtype, in
         const size_t npub = (size_t)sp.n_qtiles * TILE_Q * sp.splits * KP;
         if ((e = h->pub.ensure(npub * 4)) != hipSuccess) return e;
         sp.pub = (float*)h->pub.p;
-        // union bound taken at rank max(3k/2, 16) (<= KP): tighter pruning;
+        // union bound taken at rank max(6k/5, 12) (<= KP): tighter pruning;
         // the refine's certification bound is capped by the final threshold.
-        // (k = 10: 16, was 20 -- config (b) -2.4 %, 0 fallbacks,
-        // profiles/r3/ab/knobs)
-        sp.prune_rank = h->opt.prune_rank > 0 ? h->opt.prune_rank : std::max(3 * k / 2, 16);
+        // (k = 10: 12, was 20 -- config (b) -4.5 %, (d) -1 %, 0 fallbacks in
+        // every certification stress case; profiles/r3/ab/prune_rank*)
+        sp.prune_rank = h->opt.prune_rank > 0 ? h->opt.prune_rank : std::max(6 * k / 5, 12);
         sp.prune_rank = std::max(k, std::min(KP, sp.prune_rank));
     }
     P.ncand = (size_t)sp.n_qtiles * sp.splits * TILE_Q * KP;

@@ -88,15 +88,17 @@ int fx_index_set_normalize(FxIndex* index, int on);
  * stream waits (on the device, no host sync) for the work already enqueued on
  * the previous one. */
 int fx_index_set_stream(FxIndex* index, void* stream);
-/* Per-index tuning / diagnostic option (name -> integer value).  Initial
+/* Per-index tuning option (name -> integer value).  Initial
  * values come from the FX_* environment variables, read once at index
- * creation; nothing on the search path reads the environment.  Names:
- * "search_graph" (replay small host searches as one hipGraph), "force_fallback"
- * (test hook: every query through the exact fallback), "scan_place",
- * "scan_sx", "reduce_cand", "f32_split", "centre", "scan_pub", "prune_rank",
- * "compact_at" (list fill that triggers a compaction), "union_w" (splits per
- * union-bound window), "scan_dbg" (see DESIGN.md 3).  Unknown name:
- * FX_E_ARG. */
+ * creation; nothing on the search path reads the environment.  Names and
+ * accepted values: "search_graph" 0/1 (replay small host searches as one
+ * hipGraph), "scan_place" -1/0/1, "scan_sx" >= 0, "reduce_cand" 0/1,
+ * "f32_split" 0/1, "centre" 0/1, "scan_pub" 0/1, "prune_rank" 0..32,
+ * "compact_at" 0 or 33..64 (list fill that triggers a compaction), "union_w"
+ * 0/16/32/64 (splits per union-bound window).  None changes results, only
+ * speed.  Unknown name or out-of-range value: FX_E_ARG.  (The diagnostic
+ * build libfx_index_diag.so adds test hooks -- "force_fallback",
+ * "scan_dbg" -- that the product library does not have.) */
 int fx_index_set_option(FxIndex* index, const char* name, int64_t value);
 /* Global id of local row 0 (row-sharded multi-GPU: shard offset). */
 int fx_index_set_id_offset(FxIndex* index, int64_t offset);
@@ -133,6 +135,13 @@ int fx_index_last_fallbacks(FxIndex* index, int64_t* out);
 /* Of those, the queries the re-scan could not certify either, re-ranked by
  * the exact fp64 scan of every row. */
 int fx_index_last_exact_fallbacks(FxIndex* index, int64_t* out);
+/* Candidate-list integrity of the last search: entries the exact re-rank
+ * dropped because their row id (other than the empty-slot -1) lay outside
+ * [0, ntotal).  Always 0 unless a scan list was corrupted; the dropped
+ * entries are never gathered, so a non-zero count means the top-k may be
+ * missing rows and must be treated as an error by the caller (faiss itself
+ * cannot return such a result: faiss_store.py:64). */
+int fx_index_last_dropped_candidates(FxIndex* index, int64_t* out);
 
 /* IndexFlatL2 reset (faiss_store.py:124-128). Keeps the HBM allocation. */
 int fx_index_reset(FxIndex* index);
@@ -150,7 +159,8 @@ int fx_index_read(const char* path, int storage_dtype, int device, FxIndex** out
 
 /* Merge G per-shard result lists (device pointers, layout [G][nq][k], global
  * ids, each list ordered) into D_out/I_out [nq][k] under the index order
- * (L2: ascending; IP: descending; ties -> smaller id).  `stream` may be NULL. */
+ * (L2: ascending; IP: descending; ties -> smaller id).  `stream` may be NULL.
+ * k > FX_MAX_K merges at most 64 shards (FX_E_UNSUPPORTED beyond). */
 int fx_merge_shards(int metric, int nshards, int64_t nq, int k, const float* D_in,
                     const int64_t* I_in, float* D_out, int64_t* I_out, int device, void* stream);
 

@@ -27,8 +27,6 @@ try:  # pragma: no cover - torch is part of the image
 except Exception:  # noqa: BLE001
     pass
 
-lib = ctypes.CDLL(str(LIB_PATH))
-
 F32, BF16, F16 = 0, 1, 2
 METRIC_INNER_PRODUCT, METRIC_L2 = 0, 1
 MEM_HOST, MEM_DEVICE = 0, 1
@@ -58,6 +56,7 @@ SIGNATURES = {
     "fx_index_search": (_i, [_vp, _i64, _vp, _i, _i, _i, _vp, _vp, _i]),
     "fx_index_last_fallbacks": (_i, [_vp, ctypes.POINTER(_i64)]),
     "fx_index_last_exact_fallbacks": (_i, [_vp, ctypes.POINTER(_i64)]),
+    "fx_index_last_dropped_candidates": (_i, [_vp, ctypes.POINTER(_i64)]),
     "fx_index_reset": (_i, [_vp]),
     "fx_index_reconstruct_n": (_i, [_vp, _i64, _i64, _vp]),
     "fx_index_write": (_i, [_vp, ctypes.c_char_p]),
@@ -69,33 +68,46 @@ SIGNATURES = {
                                    ctypes.POINTER(_i64)]),
 }
 
-# FX_INDEX_LIB selects another build (same-box A/B of an older library): a
-# symbol that build predates is left unbound instead of failing the import;
-# the in-tree library must export every symbol
-_AB_BUILD = "FX_INDEX_LIB" in os.environ
-for _name, (_res, _args) in SIGNATURES.items():
-    try:
-        _fn = getattr(lib, _name)
-    except AttributeError:
-        if not _AB_BUILD:
-            raise
-        continue
-    _fn.restype = _res
-    _fn.argtypes = _args
+
+def bind(path: Path, ab_build: bool = False) -> ctypes.CDLL:
+    """Load one build of the library and declare every signature.  An A/B
+    build (FX_INDEX_LIB: an older library on the same box) may predate a
+    symbol, which is then left unbound; any other build must export all."""
+    so = ctypes.CDLL(str(path))
+    for name, (res, args) in SIGNATURES.items():
+        try:
+            fn = getattr(so, name)
+        except AttributeError:
+            if not ab_build:
+                raise
+            continue
+        fn.restype = res
+        fn.argtypes = args
+    return so
+
+
+lib = bind(LIB_PATH, ab_build="FX_INDEX_LIB" in os.environ)
+
+# The diagnostic build (make -C csrc diag): the same kernels with test hooks
+# (force_fallback, the scan's key dump) in its option table.  Loaded only by
+# rag_faiss_embedding_amd.diag (tests); the product never touches it.
+DIAG_PATH = _HERE / "libfx_index_diag.so"
 
 
 class FxError(RuntimeError):
     """A failure reported by the HIP library (faiss raises RuntimeError)."""
 
 
-def last_error() -> str:
-    msg = lib.fx_last_error()
+def last_error(so: ctypes.CDLL = None) -> str:
+    msg = (so or lib).fx_last_error()
     return msg.decode("utf-8", "replace") if msg else ""
 
 
-def check(rc: int) -> None:
+def check(rc: int, so: ctypes.CDLL = None) -> None:
+    """Raise the library's thread-local message (of the build `so` that
+    returned rc; default the product library) when rc != 0."""
     if rc != 0:
-        raise FxError(last_error() or f"fx error {rc}")
+        raise FxError(last_error(so) or f"fx error {rc}")
 
 
 def device_count() -> int:

@@ -245,7 +245,7 @@ hipError_t launch_hugek_search(const HugeKParams& p, void* ws, size_t ws_bytes, 
 // (-D, id) for IP; missing entries I = -1 last), so the merged top k is a
 // G-way merge: one thread per query keeps the G list heads and emits the
 // smallest k times (O(k G) per query; the rare large-k path).
-constexpr int HKM_MAXG = 64;
+constexpr int HKM_MAXG = FX_HUGEK_MAX_SHARDS;
 
 __global__ __launch_bounds__(64) void k_hkm_merge(int nshards, int64_t nq, int k, int metric,
                                                   const float* __restrict__ D_in, const int64_t* __restrict__ I_in,

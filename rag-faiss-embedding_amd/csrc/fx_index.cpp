@@ -79,12 +79,13 @@ struct DevBuf {
 
 inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
-// Per-index tuning and diagnostic options.  Initial values come from the
-// FX_* environment variables, read ONCE when the index is created (never on
-// the search path); fx_index_set_option changes them afterwards.
+// Per-index tuning options.  Initial values come from the FX_* environment
+// variables, read ONCE when the index is created (never on the search path);
+// fx_index_set_option changes them afterwards (range-checked: opt_range).
+// Test hooks and diagnostic dumps exist only in the diagnostic build
+// (-DFX_DIAG: libfx_index_diag.so, make diag / abl), never in libfx_index.so.
 struct Options {
     int search_graph = 0;    // FX_SEARCH_GRAPH: replay small host searches as one hipGraph
-    int force_fallback = 0;  // FX_FORCE_FALLBACK: flag every query (test hook of the exact fallback)
     int place = -1;          // FX_SCAN_PLACE: scan block placement (-1 automatic, 0, 1)
     int sx = 0;              // FX_SCAN_SX: corpus splits per XCD under placement 1 (0 automatic)
     int reduce_cand = 1;     // FX_REDUCE_CAND: merge 16 splits' lists before the refine (small nq)
@@ -94,9 +95,14 @@ struct Options {
     int prune_rank = 0;      // FX_PRUNE_RANK: rank of the shared threshold (0: max(6k/5, 12))
     int compact_at = 0;      // FX_COMPACT_AT: list fill that triggers a compaction (0: default, KP < v <= CAP)
     int union_w = 0;         // FX_UNION_W: splits per union-bound window (16, 32, 64; 0: by split count)
-    int scan_dbg = 0;        // FX_SCAN_DBG: ablation switches of -DFX_ABLATION builds / key dump (32)
     int graph_verbose = 0;   // FX_SEARCH_GRAPH_VERBOSE
+#ifdef FX_DIAG
+    int force_fallback = 0;  // FX_FORCE_FALLBACK: flag every query (1: -> re-scan, 2: -> exact scan)
+    int scan_dbg = 0;        // FX_SCAN_DBG: ablation switches of -DFX_ABLATION builds / key dump (32)
     std::string trace, stamps, cand, keys;  // FX_SCAN_TRACE / _STAMPS / _CAND / _KEYS dump paths
+#else
+    static constexpr int force_fallback = 0, scan_dbg = 0;
+#endif
 
     void from_env() {
         auto num = [](const char* name, int& v) {
@@ -106,7 +112,6 @@ struct Options {
             if (const char* e = getenv(name); e && *e) v = e;
         };
         num("FX_SEARCH_GRAPH", search_graph);
-        num("FX_FORCE_FALLBACK", force_fallback);
         num("FX_SCAN_PLACE", place);
         num("FX_SCAN_SX", sx);
         num("FX_REDUCE_CAND", reduce_cand);
@@ -116,20 +121,57 @@ struct Options {
         num("FX_PRUNE_RANK", prune_rank);
         num("FX_COMPACT_AT", compact_at);
         num("FX_UNION_W", union_w);
-        num("FX_SCAN_DBG", scan_dbg);
         num("FX_SEARCH_GRAPH_VERBOSE", graph_verbose);
+        (void)str;
+#ifdef FX_DIAG
+        num("FX_FORCE_FALLBACK", force_fallback);
+        num("FX_SCAN_DBG", scan_dbg);
         str("FX_SCAN_TRACE", trace);
         str("FX_SCAN_STAMPS", stamps);
         str("FX_SCAN_CAND", cand);
         str("FX_SCAN_KEYS", keys);
+#endif
     }
-    int* find(const char* name) {
-        static const char* names[] = {"search_graph", "force_fallback", "scan_place", "scan_sx", "reduce_cand",
-                                      "f32_split", "centre", "scan_pub", "prune_rank", "scan_dbg", "compact_at", "union_w"};
-        int* slots[] = {&search_graph, &force_fallback, &place, &sx, &reduce_cand,
-                        &f32_split, &centre, &pub, &prune_rank, &scan_dbg, &compact_at, &union_w};
-        for (int i = 0; i < (int)(sizeof(names) / sizeof(names[0])); ++i)
-            if (strcmp(name, names[i]) == 0) return slots[i];
+    // option name -> its slot and accepted range [lo, hi] (allowed: a value
+    // list when `set` is non-null)
+    struct Slot {
+        const char* name;
+        int* v;
+        int lo, hi;
+        const int* set;
+        int nset;
+    };
+    int* find(const char* name, int64_t value, const char** why) {
+        static const int kWindows[] = {0, 16, 32, 64};
+        const Slot slots[] = {
+            {"search_graph", &search_graph, 0, 1, nullptr, 0},
+            {"scan_place", &place, -1, 1, nullptr, 0},
+            {"scan_sx", &sx, 0, 1 << 16, nullptr, 0},
+            {"reduce_cand", &reduce_cand, 0, 1, nullptr, 0},
+            {"f32_split", &f32_split, 0, 1, nullptr, 0},
+            {"centre", &centre, 0, 1, nullptr, 0},
+            {"scan_pub", &pub, 0, 1, nullptr, 0},
+            {"prune_rank", &prune_rank, 0, KP, nullptr, 0},
+            {"compact_at", &compact_at, 0, CAP, nullptr, 0},
+            {"union_w", &union_w, 0, 64, kWindows, 4},
+#ifdef FX_DIAG
+            {"force_fallback", &force_fallback, 0, 2, nullptr, 0},
+            {"scan_dbg", &scan_dbg, 0, 1 << 20, nullptr, 0},
+#endif
+        };
+        for (const Slot& sl : slots) {
+            if (strcmp(name, sl.name) != 0) continue;
+            bool ok = value >= sl.lo && value <= sl.hi;
+            if (ok && sl.set) {
+                ok = false;
+                for (int i = 0; i < sl.nset; ++i) ok |= value == sl.set[i];
+            }
+            // compact_at: 0 (default) or a fill in (KP, CAP]
+            if (ok && sl.v == &compact_at) ok = value == 0 || value > KP;
+            *why = ok ? nullptr : "value out of range";
+            return sl.v;
+        }
+        *why = "unknown option";
         return nullptr;
     }
 };
@@ -190,9 +232,13 @@ struct FxIndex {
     int64_t last_fallbacks = 0;
     // uncertified count of the last search, copied stream-ordered into pinned
     // memory; read (after a stream sync) only when asked for (fb_pending)
-    int* pin_nf = nullptr;  // [0] queries re-scanned, [1] queries sent to the exact scan
+    int* pin_nf = nullptr;  // [0] queries re-scanned, [1] queries sent to the exact scan, [2] dropped ids
     bool fb_pending = false;
     int64_t last_exact = 0;
+    // candidate entries the refine dropped for a row id outside [0, ntotal)
+    // (a corrupted candidate list; 0 unless something is broken)
+    int64_t last_dropped = 0;
+    int* dev_drop = nullptr;  // its device word, zeroed at the start of every search
     // profiling
     bool profile = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_scan, ev_merge;
@@ -325,8 +371,8 @@ bool use_reduce(const FxIndex* h, int k, int64_t nq, int splits) {
 
 hipError_t ensure_pinned_count(FxIndex* h) {
     if (h->pin_nf) return hipSuccess;
-    hipError_t e = hipHostMalloc((void**)&h->pin_nf, 2 * sizeof(int), hipHostMallocDefault);
-    if (e == hipSuccess) h->pin_nf[0] = h->pin_nf[1] = 0;
+    hipError_t e = hipHostMalloc((void**)&h->pin_nf, 3 * sizeof(int), hipHostMallocDefault);
+    if (e == hipSuccess) h->pin_nf[0] = h->pin_nf[1] = h->pin_nf[2] = 0;
     return e;
 }
 
@@ -405,6 +451,7 @@ struct SearchPlan {
     RefineParams rp2{};
     PrepParams pp2{};
     int* n_exact = nullptr;  // queries the re-scan left uncertified too (-> exact scan)
+    int64_t nq_rescan = 0;   // flagged queries the re-scan takes (the rest: exact scan)
 };
 
 // The re-scan of the queries pass 1 could not certify (rows flag_list[0 ..
@@ -414,20 +461,27 @@ struct SearchPlan {
 // certification bound sits near the k1-th key instead of the ~2k-th.  Its
 // uncertified queries go to the exact scan.  Launched always; every kernel
 // reads the flagged count and exits at once when it is 0.
+// The re-scan's workspace is sized for at most RESCAN_MAX flagged queries,
+// whatever the batch (its lists are k1/4 splits wide): flagged queries past
+// that go straight to the exact scan (k_rescan_overflow), so a large batch
+// never pays for a re-scan workspace it almost never uses.
 hipError_t plan_rescan(FxIndex* h, SearchPlan& P) {
     hipError_t e;
-    const int64_t nq = P.nq;
+    const int64_t nq = std::min<int64_t>(P.nq, RESCAN_MAX), nq_pad = round_up(nq, QPAD);
     const int k1 = std::min(2 * FX_BIG_K, std::max(512, 4 * P.k));
     int* n_flag = P.rp.n_flag;
-    if ((e = h->rq_f32.ensure((size_t)P.nq_pad * h->kdim * 4)) != hipSuccess) return e;
-    if ((e = h->rq_op.ensure((size_t)P.nq_pad * h->row_bytes)) != hipSuccess) return e;
+    if ((e = h->rq_f32.ensure((size_t)nq_pad * h->kdim * 4)) != hipSuccess) return e;
+    if ((e = h->rq_op.ensure((size_t)nq_pad * h->row_bytes)) != hipSuccess) return e;
     if ((e = h->rq_eps.ensure((size_t)nq * 4)) != hipSuccess) return e;
     if ((e = h->rq_rho.ensure((size_t)nq * 4)) != hipSuccess) return e;
     if ((e = h->rq_shift.ensure((size_t)nq * 8)) != hipSuccess) return e;
-    if ((e = h->rq_gtau.ensure((size_t)P.nq_pad * 4)) != hipSuccess) return e;
-    if ((e = h->rq_flag.ensure((size_t)(nq + 1) * 4)) != hipSuccess) return e;
+    if ((e = h->rq_gtau.ensure((size_t)nq_pad * 4)) != hipSuccess) return e;
+    if ((e = h->rq_flag.ensure((size_t)(P.nq + 1) * 4)) != hipSuccess) return e;  // every query may go exact
+    P.nq_rescan = nq;
     PrepParams& pp = P.pp2;
     pp = P.pp;
+    pp.nq = nq;
+    pp.nq_pad = nq_pad;
     pp.q = h->qf32.p;  // pass 1's fp32 copy of the batch, rows padded to kdim
     pp.q_dt = F32;
     pp.d = h->kdim;
@@ -440,6 +494,7 @@ hipError_t plan_rescan(FxIndex* h, SearchPlan& P) {
     pp.qshift = (double*)h->rq_shift.p;
     ScanParams& sp = P.sp2;
     sp = P.sp;
+    sp.nq = nq;
     plan_scan(h, nq, k1, sp);  // k1 > KP: share = 0, >= k1/4 splits
     sp.qop = (const char*)h->rq_op.p;
     sp.gtau = (unsigned*)h->rq_gtau.p;
@@ -457,6 +512,7 @@ hipError_t plan_rescan(FxIndex* h, SearchPlan& P) {
     sp.cand_i = (int*)h->rq_cand_i.p;
     RefineParams& rp = P.rp2;
     rp = P.rp;
+    rp.nq = nq;
     rp.cand_d = sp.cand_d;
     rp.cand_i = sp.cand_i;
     rp.splits = sp.splits;
@@ -564,6 +620,7 @@ hipError_t plan_search(FxIndex* h, int64_t nq, const void* qdev, int q_dtype, in
     rp.I = Id;
     rp.n_flag = (int*)h->flag.p;
     rp.flag_list = rp.n_flag + 1;
+    rp.n_drop = h->dev_drop;
     // small batches: one wave per query walks splits * KP candidates (256 splits
     // at nq = 1); issue 4 chunks of loads at a time (nq = 1: 0.84 -> ~0.3 ms)
     rp.prefetch = nq <= 256 ? 4 : 1;
@@ -590,6 +647,7 @@ hipError_t plan_search(FxIndex* h, int64_t nq, const void* qdev, int q_dtype, in
 hipError_t enqueue_search(FxIndex* h, SearchPlan& P, hipStream_t s, bool timed, hipEvent_t* ev) {
     hipError_t e;
     if ((e = launch_prep_queries(P.pp, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(P.rp.n_drop, 0, 4, s)) != hipSuccess) return e;
     if ((e = hipMemsetD32Async((hipDeviceptr_t)P.sp.gtau, 0xff800000u, (size_t)P.nq_pad, s)) != hipSuccess)
         return e;  // ord(+inf)
     if (P.sp.pub) {
@@ -604,7 +662,7 @@ hipError_t enqueue_search(FxIndex* h, SearchPlan& P, hipStream_t s, bool timed, 
     if (P.reduce) {
         int ng = 0;
         if ((e = launch_reduce_cand(P.sp.cand_d, P.sp.cand_i, P.sp.splits, P.nq, P.sp.n_qtiles, (float*)h->cand2_d.p,
-                                    (int*)h->cand2_i.p, &ng, s)) != hipSuccess)
+                                    (int*)h->cand2_i.p, &ng, P.rp.ntotal, P.rp.n_drop, s)) != hipSuccess)
             return e;
         rp.cand_d = (const float*)h->cand2_d.p;
         rp.cand_i = (const int*)h->cand2_i.p;
@@ -618,18 +676,24 @@ hipError_t enqueue_search(FxIndex* h, SearchPlan& P, hipStream_t s, bool timed, 
     // certify is re-ranked by the exact scan.  Decided on the device: these
     // kernels are always enqueued and exit at once when nothing was flagged,
     // so no host round trip sits inside the search.
-    if (P.sp.dbg != 0) return hipSuccess;
+#ifdef FX_ABLATION
+    if ((P.sp.dbg & ~32) != 0) return hipSuccess;  // ablated scans: results invalid, no fallback chain
+#endif
     if ((e = launch_prep_queries(P.pp2, s)) != hipSuccess) return e;
     if ((e = hipMemsetD32Async((hipDeviceptr_t)P.sp2.gtau, 0xff800000u, (size_t)P.nq_pad, s)) != hipSuccess)
         return e;
     if ((e = launch_scan(P.scan_dt, h->metric, P.sp2, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(P.n_exact, 0, 4, s)) != hipSuccess) return e;
+    if (P.nq_rescan < P.nq &&
+        (e = launch_rescan_overflow(P.rp.n_flag, (int)P.nq_rescan, P.n_exact, s)) != hipSuccess)
+        return e;
     if ((e = launch_refine(h->dtype, h->metric, P.rp2, s)) != hipSuccess) return e;
     return launch_exact_fallback(h->dtype, h->metric, h->codes, h->row_bytes, h->kdim, h->ntotal, P.rp.qf32,
                                  P.n_exact, P.k, h->id_offset, (float*)h->fbc_d.p, (int*)h->fbc_i.p, P.rp.D, P.rp.I,
                                  s);
 }
 
+#ifdef FX_DIAG
 template <typename T>
 hipError_t dump_device(const std::string& path, const void* dev, size_t n) {
     std::vector<T> v(n);
@@ -641,6 +705,7 @@ hipError_t dump_device(const std::string& path, const void* dev, size_t n) {
     }
     return hipSuccess;
 }
+#endif
 
 int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int k, float* D, int64_t* I,
               int out_mem) {
@@ -664,6 +729,7 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
     HIP_TRY(update_scan_image(h));
     SearchPlan P;
     HIP_TRY(plan_search(h, nq, qdev, q_dtype, k, Dd, Id, P));
+#ifdef FX_DIAG
     // diagnostics (Options): per-block placement/timing, phase stamps, the
     // scan's key matrix, raw candidate lists -> binary files
     const size_t grid = (size_t)P.sp.grid;
@@ -683,6 +749,7 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
         HIP_TRY(hipMemsetAsync(h->trace.p, 0, grid * 32, s));
         P.sp.trace = (unsigned long long*)h->trace.p;
     }
+#endif
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     if (h->profile)
         for (auto& x : ev) HIP_TRY(hipEventCreate(&x));
@@ -693,9 +760,10 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
     }
     HIP_TRY(ensure_pinned_count(h));
     HIP_TRY(hipMemcpyAsync(h->pin_nf, P.rp.n_flag, 4, hipMemcpyDeviceToHost, s));
-    if (P.sp.dbg == 0) HIP_TRY(hipMemcpyAsync(h->pin_nf + 1, P.n_exact, 4, hipMemcpyDeviceToHost, s));
-    else h->pin_nf[1] = 0;
+    HIP_TRY(hipMemcpyAsync(h->pin_nf + 1, P.n_exact, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(h->pin_nf + 2, P.rp.n_drop, 4, hipMemcpyDeviceToHost, s));
     h->fb_pending = true;
+#ifdef FX_DIAG
     if (!h->opt.cand.empty()) {
         HIP_TRY(hipStreamSynchronize(s));
         HIP_TRY(dump_device<float>(h->opt.cand, P.sp.cand_d, P.ncand));
@@ -717,12 +785,14 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
         if (FILE* f = fopen(h->opt.trace.c_str(), "wb")) fclose(f);
         HIP_TRY(dump_device<unsigned long long>(h->opt.trace, P.sp.trace, grid * 4));
     }
+#endif
     if (out_mem == FX_MEM_HOST) {
         HIP_TRY(hipMemcpyAsync(D, Dd, (size_t)nq * k * 4, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipMemcpyAsync(I, Id, (size_t)nq * k * 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         h->last_fallbacks = h->pin_nf[0];
         h->last_exact = h->pin_nf[1];
+        h->last_dropped = h->pin_nf[2];
         h->fb_pending = false;
     }
     return FX_OK;
@@ -767,8 +837,13 @@ int do_search_hugek(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_me
     p.D = Dd;
     p.I = Id;
     HIP_TRY(launch_hugek_search(p, h->hk_ws.p, h->hk_ws.bytes, qb, s));
+    // the sort keys (up to 2 GiB + rocPRIM temporaries) are not kept past the
+    // call: k > FX_MAX_K is the rare caller's path (hipFree waits for the stream)
+    HIP_TRY(hipStreamSynchronize(s));
+    h->hk_ws.release();
     h->last_fallbacks = 0;
     h->last_exact = 0;
+    h->last_dropped = 0;
     h->fb_pending = false;
     if (out_mem == FX_MEM_HOST) {
         HIP_TRY(hipMemcpyAsync(D, Dd, (size_t)nq * k * 4, hipMemcpyDeviceToHost, s));
@@ -832,7 +907,7 @@ hipError_t graph_build(FxIndex* h, int64_t nq, int q_dtype, int k) {
         if ((e = hipHostMalloc((void**)&h->ghI, nd * 8, hipHostMallocDefault)) != hipSuccess) return e;
         h->ghd_n = nd;
     }
-    if (!h->ghnf && (e = hipHostMalloc((void**)&h->ghnf, 8, hipHostMallocDefault)) != hipSuccess) return e;
+    if (!h->ghnf && (e = hipHostMalloc((void**)&h->ghnf, 12, hipHostMallocDefault)) != hipSuccess) return e;
     SearchPlan P;
     if ((e = plan_search(h, nq, h->qin.p, q_dtype, k, (float*)h->dws.p, (int64_t*)h->iws.p, P)) != hipSuccess)
         return e;
@@ -846,6 +921,7 @@ hipError_t graph_build(FxIndex* h, int64_t nq, int q_dtype, int k) {
     if (ce == hipSuccess) ce = hipMemcpyAsync(h->ghI, P.rp.I, nd * 8, hipMemcpyDeviceToHost, s);
     if (ce == hipSuccess) ce = hipMemcpyAsync(h->ghnf, P.rp.n_flag, 4, hipMemcpyDeviceToHost, s);
     if (ce == hipSuccess) ce = hipMemcpyAsync(h->ghnf + 1, P.n_exact, 4, hipMemcpyDeviceToHost, s);
+    if (ce == hipSuccess) ce = hipMemcpyAsync(h->ghnf + 2, P.rp.n_drop, 4, hipMemcpyDeviceToHost, s);
     g_graph_capture = false;
     hipGraph_t graph = nullptr;
     e = hipStreamEndCapture(s, &graph);  // always end the capture: the stream must leave capture mode
@@ -875,6 +951,7 @@ int graph_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int k, floa
         memcpy(I, h->ghI, (size_t)nq * k * 8);
         h->last_fallbacks = h->ghnf[0];
         h->last_exact = h->ghnf[1];
+        h->last_dropped = h->ghnf[2];
         h->fb_pending = false;
         return FX_OK;
     }
@@ -936,6 +1013,8 @@ int fx_index_create(int d, int storage_dtype, int metric, int device, FxIndex** 
     if (e == hipSuccess) e = hipEventCreateWithFlags(&h->switch_ev, hipEventDisableTiming);
     if (e == hipSuccess) e = hipMalloc(&h->max_sq_bits, 16);
     if (e == hipSuccess) e = hipMemset(h->max_sq_bits, 0, 16);
+    if (e == hipSuccess) e = hipMalloc(&h->dev_drop, 16);
+    if (e == hipSuccess) e = hipMemset(h->dev_drop, 0, 16);
     if (e != hipSuccess) {
         fx_index_free(h);
         return set_err(FX_E_HIP, "index init: %s", hipGetErrorString(e));
@@ -953,6 +1032,7 @@ void fx_index_free(FxIndex* h) {
         if (h->codes) (void)hipFree(h->codes);
         if (h->norms) (void)hipFree(h->norms);
         if (h->max_sq_bits) (void)hipFree(h->max_sq_bits);
+        if (h->dev_drop) (void)hipFree(h->dev_drop);
         for (DevBuf* b : {&h->qin, &h->qf32, &h->qop, &h->qeps, &h->cand_d, &h->cand_i, &h->dws, &h->iws, &h->flag,
                           &h->fbc_d, &h->fbc_i, &h->stage, &h->gtau, &h->trace, &h->dbgbuf, &h->split, &h->cnorms,
                           &h->centre, &h->mu_part, &h->qshift, &h->qrho, &h->stamps, &h->pub, &h->cand2_d,
@@ -999,8 +1079,10 @@ int fx_index_set_stream(FxIndex* h, void* stream) {
 int fx_index_set_option(FxIndex* h, const char* name, int64_t value) {
     if (!h || !name) return set_err(FX_E_ARG, "null argument");
     std::lock_guard<std::mutex> lk(h->mu);
-    int* slot = h->opt.find(name);
+    const char* why = nullptr;
+    int* slot = h->opt.find(name, value, &why);
     if (!slot) return set_err(FX_E_ARG, "unknown option '%s'", name);
+    if (why) return set_err(FX_E_ARG, "option '%s': %s (%lld)", name, why, (long long)value);
     *slot = (int)value;
     return FX_OK;
 }
@@ -1100,12 +1182,18 @@ int fx_index_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_me
         }
         h->last_fallbacks = 0;
         h->last_exact = 0;
+        h->last_dropped = 0;
         h->fb_pending = false;
         return FX_OK;
     }
     const Options& o = h->opt;
-    if (o.search_graph == 1 && q_mem == FX_MEM_HOST && out_mem == FX_MEM_HOST && nq <= 64 && !h->profile &&
-        o.scan_dbg == 0 && o.trace.empty() && o.cand.empty() && o.stamps.empty() && h->user_stream == nullptr)
+#ifdef FX_DIAG
+    const bool diag = o.scan_dbg != 0 || !o.trace.empty() || !o.cand.empty() || !o.stamps.empty();
+#else
+    constexpr bool diag = false;
+#endif
+    if (o.search_graph == 1 && q_mem == FX_MEM_HOST && out_mem == FX_MEM_HOST && nq <= 64 && !h->profile && !diag &&
+        h->user_stream == nullptr)
         return graph_search(h, nq, q, q_dtype, k, D, I);
     return do_search(h, nq, q, q_dtype, q_mem, k, D, I, out_mem);
 }
@@ -1118,8 +1206,18 @@ static int read_counts(FxIndex* h) {
         HIP_TRY(hipStreamSynchronize(h->stream()));
         h->last_fallbacks = h->pin_nf[0];
         h->last_exact = h->pin_nf[1];
+        h->last_dropped = h->pin_nf[2];
         h->fb_pending = false;
     }
+    return FX_OK;
+}
+
+int fx_index_last_dropped_candidates(FxIndex* h, int64_t* out) {
+    if (!h || !out) return set_err(FX_E_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(h->mu);
+    const int rc = read_counts(h);
+    if (rc != FX_OK) return rc;
+    *out = h->last_dropped;
     return FX_OK;
 }
 
@@ -1261,6 +1359,9 @@ int fx_merge_shards(int metric, int nshards, int64_t nq, int k, const float* D_i
     if (metric != FX_METRIC_L2 && metric != FX_METRIC_INNER_PRODUCT) return set_err(FX_E_ARG, "bad metric");
     DeviceGuard g(device);
     if (!g.ok) return set_err(FX_E_HIP, "hipSetDevice(%d) failed", device);
+    if (k > FX_MAX_K && nshards > FX_HUGEK_MAX_SHARDS)
+        return set_err(FX_E_UNSUPPORTED, "merge of k = %d > %d lists supports at most %d shards (got %d)", k, FX_MAX_K,
+                       FX_HUGEK_MAX_SHARDS, nshards);
     if (k > FX_MAX_K)  // stream-ordered sort merge (fx_hugek.hip)
         HIP_TRY(launch_merge_shards_sort(metric, nshards, nq, k, D_in, I_in, D_out, I_out, (hipStream_t)stream));
     else

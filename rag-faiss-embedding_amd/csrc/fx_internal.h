@@ -106,7 +106,8 @@ struct RefineParams {
     const int* out_idx;    // non-null: query q's results go to row out_idx[q] of D / I, and an
                            // uncertified q is flagged as out_idx[q] (the re-scan's gathered queries)
     int64_t ntotal;        // rows of the index: a candidate row id outside [0, ntotal) is never gathered
-                           // (defence in depth: a list bug then shows as a parity failure, not a fault)
+    int* n_drop;           // ... and counted here (ids other than -1 outside [0, ntotal): a corrupted
+                           // candidate list), read back by fx_index_last_dropped_candidates
 };
 
 // exact fallback (k_fb_scan / k_fb_merge): corpus splits per flagged query,
@@ -120,6 +121,13 @@ __host__ __device__ inline int fb_splits_for(int nf, int64_t ntotal) {
     if (s > by_rows) s = (int)by_rows;
     return s < 1 ? 1 : s;
 }
+
+// the re-scan of uncertified queries takes at most this many of them per
+// search (its workspace is sized for it); the rest go to the exact scan
+constexpr int64_t RESCAN_MAX = 2048;
+// flagged queries [cap, n_flag[0]) of a search -> the exact scan's list
+// (n_exact[0] count, list at n_exact + 1); device-gated like the fallbacks
+hipError_t launch_rescan_overflow(const int* n_flag, int cap, int* n_exact, hipStream_t s);
 
 // True on a thread that is capturing a search into a hipGraph (fx_index.cpp
 // graph_build): the scan launchers then skip hipFuncSetAttribute, which the
@@ -158,7 +166,7 @@ hipError_t launch_refine(int st_dt, int metric, const RefineParams& p, hipStream
 // small batches: merge each 16 splits' candidate lists of a query into their
 // top KP (k_reduce_cand); *ngroups = ceil(splits / 16) lists per query after
 hipError_t launch_reduce_cand(const float* cd, const int* ci, int splits, int64_t nq, int n_qtiles, float* od,
-                              int* oi, int* ngroups, hipStream_t s);
+                              int* oi, int* ngroups, int64_t ntotal, int* n_drop, hipStream_t s);
 // both fallback launches, always enqueued; they read the flagged count at
 // n_flag[0] (list at n_flag + 1) and do nothing when it is 0
 hipError_t launch_exact_fallback(int st_dt, int metric, const char* codes, int row_bytes, int kdim,
@@ -186,7 +194,8 @@ int hugek_batch(int64_t ntotal, int64_t nq);
 hipError_t hugek_workspace(int64_t ntotal, int kdim, int qb, size_t* bytes);
 hipError_t launch_hugek_search(const HugeKParams& p, void* ws, size_t ws_bytes, int qb, hipStream_t s);
 // fx_merge_shards for k > FX_BIG_K: per query, a G-way merge of the gathered
-// lists (each in the index order); at most 64 shards
+// lists (each in the index order); at most FX_HUGEK_MAX_SHARDS shards
+constexpr int FX_HUGEK_MAX_SHARDS = 64;
 hipError_t launch_merge_shards_sort(int metric, int nshards, int64_t nq, int k, const float* D_in,
                                     const int64_t* I_in, float* D_out, int64_t* I_out, hipStream_t s);
 // fp32 code rows [r0, r1) -> their F32S scan image (same row stride)

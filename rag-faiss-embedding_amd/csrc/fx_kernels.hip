@@ -756,6 +756,17 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_topk(ScanParams p) {
 // merge + exact refine + certification: one wave per query
 // ---------------------------------------------------------------------------
 // merge one chunk of 64 candidates (one per lane) into the running best-64
+// Candidate-list integrity (RefineParams.n_drop): an entry's row id is -1
+// (an empty slot) or a row of the index.  Anything else means a corrupted
+// list; it is never gathered (a fault would follow) but counted, so the
+// search reports it instead of returning a silently thinner candidate set.
+__device__ __forceinline__ int cand_id_corrupt(int ii, int64_t ntotal) { return ii != -1 && (ii < 0 || ii >= ntotal); }
+// per-lane counts -> the device word (one wave-uniform branch in the common case: none)
+__device__ __forceinline__ void count_dropped(int bad, int* n_drop, int lane) {
+    (void)lane;
+    if (__builtin_amdgcn_ballot_w64(bad != 0) != 0 && bad != 0 && n_drop) atomicAdd(n_drop, bad);
+}
+
 __device__ __forceinline__ void refine_take(float d, int i, float& bd, int& bi, float& td, int& ti, int& nvalid,
                                             int lane) {
     nvalid += __popcll(__ballot(i != INT_MAX));
@@ -779,7 +790,7 @@ __device__ __forceinline__ void refine_take(float d, int i, float& bd, int& bi, 
 template <int G>
 __global__ __launch_bounds__(256) void k_reduce_cand(const float* __restrict__ cd, const int* __restrict__ ci,
                                                      int splits, int64_t nq, int ngroups, float* __restrict__ od,
-                                                     int* __restrict__ oi) {
+                                                     int* __restrict__ oi, int64_t ntotal, int* __restrict__ n_drop) {
     const int lane = threadIdx.x & 63;
     const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int64_t q = w / ngroups;
@@ -790,6 +801,7 @@ __global__ __launch_bounds__(256) void k_reduce_cand(const float* __restrict__ c
     constexpr int NL = G * KP / 64;  // loads per lane
     float dv[NL];
     int iv[NL];
+    int bad = 0;
 #pragma unroll
     for (int u = 0; u < NL; ++u) {
         const int c = u * 64 + lane, s = c / KP, j = c - s * KP;
@@ -799,9 +811,11 @@ __global__ __launch_bounds__(256) void k_reduce_cand(const float* __restrict__ c
             const int64_t off = (((int64_t)qtile * splits + s0 + s) * TILE_Q + qq) * KP + j;
             const int ii = ci[off];
             const float dd = cd[off];
-            if (ii >= 0) { dv[u] = dd; iv[u] = ii; }
+            if (ii >= 0 && ii < ntotal) { dv[u] = dd; iv[u] = ii; }
+            else bad += cand_id_corrupt(ii, ntotal);
         }
     }
+    count_dropped(bad, n_drop, lane);
     float bd = FX_INF, td = FX_INF;
     int bi = INT_MAX, ti = INT_MAX, nvalid = 0;
 #pragma unroll
@@ -813,14 +827,29 @@ __global__ __launch_bounds__(256) void k_reduce_cand(const float* __restrict__ c
     }
 }
 
+// flagged queries past the re-scan's capacity go straight to the exact scan
+__global__ __launch_bounds__(256) void k_rescan_overflow(const int* __restrict__ n_flag, int cap,
+                                                         int* __restrict__ n_exact) {
+    const int nf = n_flag[0];
+    for (int i = cap + (int)(blockIdx.x * blockDim.x + threadIdx.x); i < nf; i += (int)(gridDim.x * blockDim.x)) {
+        const int pos = atomicAdd(n_exact, 1);
+        n_exact[1 + pos] = n_flag[1 + i];
+    }
+}
+
+hipError_t launch_rescan_overflow(const int* n_flag, int cap, int* n_exact, hipStream_t s) {
+    hipLaunchKernelGGL(k_rescan_overflow, dim3(64), dim3(256), 0, s, n_flag, cap, n_exact);
+    return hipGetLastError();
+}
+
 hipError_t launch_reduce_cand(const float* cd, const int* ci, int splits, int64_t nq, int n_qtiles, float* od,
-                              int* oi, int* ngroups, hipStream_t s) {
+                              int* oi, int* ngroups, int64_t ntotal, int* n_drop, hipStream_t s) {
     constexpr int G = 16;
     *ngroups = (splits + G - 1) / G;
     (void)n_qtiles;
     const int64_t waves = nq * (int64_t)*ngroups;
     hipLaunchKernelGGL((k_reduce_cand<G>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, cd, ci, splits, nq,
-                       *ngroups, od, oi);
+                       *ngroups, od, oi, ntotal, n_drop);
     return hipGetLastError();
 }
 
@@ -857,7 +886,7 @@ __global__ __launch_bounds__(256) void k_refine(RefineParams p) {
     // ---- phase 1: KP smallest approx keys over all splits (running best-64)
     float bd = FX_INF, td = FX_INF;
     int bi = INT_MAX, ti = INT_MAX;
-    int nvalid = 0;
+    int nvalid = 0, bad = 0;
     if constexpr (PF > 1) {
         for (int base = 0; base < ncand; base += 64 * PF) {
             float dv[PF];
@@ -873,6 +902,7 @@ __global__ __launch_bounds__(256) void k_refine(RefineParams p) {
                     const float dd = p.cand_d[off];  // both loads in flight together
                     const int ii = p.cand_i[off];
                     if (ii >= 0 && ii < p.ntotal) { dv[u] = dd; iv[u] = ii; }
+                    else bad += cand_id_corrupt(ii, p.ntotal);
                 }
             }
 #pragma unroll
@@ -888,6 +918,7 @@ __global__ __launch_bounds__(256) void k_refine(RefineParams p) {
                 const int64_t off = (((int64_t)qtile * p.splits + s) * TILE_Q + qq) * KP + j;
                 const int ii = p.cand_i[off];
                 if (ii >= 0 && ii < p.ntotal) { d = p.cand_d[off]; i = ii; }
+                else bad += cand_id_corrupt(ii, p.ntotal);
             }
             nvalid += __popcll(__ballot(i != INT_MAX));
             const bool pass = i != INT_MAX && key_lt(d, i, td, ti);
@@ -899,6 +930,8 @@ __global__ __launch_bounds__(256) void k_refine(RefineParams p) {
             ti = __shfl(bi, KP - 1, 64);
         }
     }
+
+    count_dropped(bad, p.n_drop, lane);
 
     // ---- phase 2: exact fp64 values of the KP selected rows (16 lanes / row)
     const float* xq = p.qf32 + q * (int64_t)p.kdim;
@@ -988,6 +1021,8 @@ __global__ __launch_bounds__(BT_THREADS) void k_refine_big(RefineParams p) {
                 i = ii;
                 valid = true;
                 if (j == KP - 1) atomicMin(&t_split, f2ord(d));  // a full split's KP-th key
+            } else if (cand_id_corrupt(ii, p.ntotal) && p.n_drop) {
+                atomicAdd(p.n_drop, 1);
             }
         }
         bt_round(sd, si, &st, K1, B, d, i, valid);

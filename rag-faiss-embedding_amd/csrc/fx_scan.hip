@@ -35,28 +35,14 @@
 
 #include <stdlib.h>
 
-// bisect switches of experimental builds
-#ifndef FX_V4_MIDWAIT
-#define FX_V4_MIDWAIT 1   // 1: one lgkmcnt(0) mid-stage; 0: counted waits per MFMA pair (no gain measured)
-#endif
-#ifndef FX_V4_LATEMIN
-#define FX_V4_LATEMIN 1   // 1: group minima after the tile; 0: beside its last MFMAs (no gain measured)
-#endif
-#ifndef FX_V4_DMAPOS
-#define FX_V4_DMAPOS 0    // MFMA pairs after which a stage's corpus pieces issue: 0 (4,6 | 4,5), 1 (1,5 | 1,5),
-#endif                    // 2 (2,6 | 2,6), 3 (3,7 | 3,7)
-
 namespace fx {
 
-// DMA ring slots (NS - 1 stages in flight): FX_V4_NS6 = 1 gives 6 where a
-// tile has >= 5 stages (needs LCAP <= 56 for the LDS), else 5.  Measured:
-// the deeper ring did not shorten the waits (they are barrier skew behind
-// slow-path tiles, not DMA latency) -- 5 slots is the default
-#ifndef FX_V4_NS6
-#define FX_V4_NS6 0
-#endif
+// DMA ring slots (NS - 1 stages in flight).  Measured: a
+// 6-slot ring (with 56-entry lists to fit the LDS), counted per-pair LDS
+// waits instead of the mid-stage lgkmcnt(0), group minima beside the last
+// MFMAs and other DMA issue points were all no faster
 template <int KSTEPS>
-constexpr int ring_slots() { return (FX_V4_NS6 && KSTEPS / 2 >= 5) ? 6 : 5; }
+constexpr int ring_slots() { return 5; }
 constexpr int S_STAGE = TILE_R * STAGE_B;       // 16 KiB = 128 rows x 128 B
 // norm / threshold slots first: every ring piece's LDS address is then >= 4 KiB,
 // more than any instruction offset subtracted from its M0 (see dma_piece)
@@ -261,9 +247,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
             // VMEM ops younger than stage g+1's: stages g+2 .. g+NS-2, issued
             // in the NS-3 stages before this one (4 corpus pieces each, + the
             // norm piece with a tile's first stage)
-            constexpr int W = 4 * (NS - 3) + ((j + 2) % SPT == 0) + ((j + 3) % SPT == 0) +
-                              (NS >= 6 && (j + 4) % SPT == 0);
-            static_assert(NS == 5 || NS == 6, "wait count written for 5 or 6 slots");
+            constexpr int W = 4 * (NS - 3) + ((j + 2) % SPT == 0) + ((j + 3) % SPT == 0);
+            static_assert(NS == 5, "wait count written for 5 slots");
             uint64_t s_a = 0, s_b = 0, s_c = 0;
             if constexpr (ABL & 64) {
                 s_a = __builtin_amdgcn_s_memtime();
@@ -309,11 +294,9 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                         static_for<4>([&](auto W) { piece(W, JP{}, NXT{}, c4, tnext); });
                         if constexpr (jp == 0) piece(std::integral_constant<int, 4>{}, JP{}, NXT{}, c4, tnext);
                     }
-                } else {
-                    constexpr int P0 = FX_V4_DMAPOS == 0 ? 4 : FX_V4_DMAPOS;
-                    constexpr int P1 = FX_V4_DMAPOS == 0 ? 6 : FX_V4_DMAPOS + 4;
-                    if constexpr (m == P0) piece(std::integral_constant<int, 0>{}, JP{}, NXT{}, c4, tnext);
-                    if constexpr (m == P1) piece(std::integral_constant<int, 1>{}, JP{}, NXT{}, c4, tnext);
+                } else {  // a stage's corpus pieces after MFMA pairs 4, 6 (half 0) and 4, 5 (half 1)
+                    if constexpr (m == 4) piece(std::integral_constant<int, 0>{}, JP{}, NXT{}, c4, tnext);
+                    if constexpr (m == 6) piece(std::integral_constant<int, 1>{}, JP{}, NXT{}, c4, tnext);
                 }
             });
             if constexpr (HI) {  // hi * x_lo (>= 14 MFMAs after each accumulator's previous write)
@@ -333,9 +316,9 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                 s_c = __builtin_amdgcn_s_memtime();
                 stq[1] += s_c - s_b;
             }
-            // (no stage-wide LDS wait here: half 1 waits for each Y[m] just
-            // before its MFMAs, counted)
-            if constexpr (FX_V4_MIDWAIT && !(ABL & 32)) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            // half 1's fragments (and in a tile's last stage the norm and
+            // threshold reads) landed
+            if constexpr (!(ABL & 32)) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (ABL & 64) {
                 const uint64_t s_d = __builtin_amdgcn_s_memtime();
@@ -346,25 +329,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
             const uint32_t rd_next = lds_base + S_RING_OFF + c1 * S_STAGE + rd_lane;
             static_for<M>([&](auto MM) {
                 constexpr int m = decltype(MM)::value;
-                // Y[m] landed: LDS ops issued after it are Y[m+1..M-1], in the
-                // last stage of a tile the 8 norm reads and 4 threshold reads
-                // of half 0, and the X reads of this half so far (2 per pair
-                // over its first four pairs); lgkmcnt holds at most 15
-                constexpr int LW = (M - 1 - m) + (LAST ? M + 2 * N : 0) + 2 * (m < M / 2 ? m : M / 2);
-                if constexpr (!(ABL & 32) && !FX_V4_MIDWAIT)
-                    asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(LW < 15 ? LW : 15) : "memory");
                 if constexpr (!(ABL & 4))
                     AsmMmaV<DT>::template mma2<0>(acc[m][0], acc[m][1], Y[m], b[kq0 + 1][0], b[kq0 + 1][1], yin[m]);
-                // last stage of the tile: acc[m - 2] is final (two MFMA pairs
-                // = 64 cycles past its last XDL write): its group minima now,
-                // beside the remaining MFMAs instead of after them
-                if constexpr (LAST && m >= 2 && !FX_V4_LATEMIN) {
-                    static_for<N>([&](auto NN) {
-                        constexpr int n = decltype(NN)::value;
-                        gmin[n][m - 2] = min4(acc[m - 2][n]);
-                    });
-                    __builtin_amdgcn_sched_barrier(0);
-                }
                 // half 0 of stage g+1: two reads per pair over the first four
                 // pairs (X[2m+1]'s last reader is >= 8 MFMAs back)
                 if constexpr (m < M / 2) {
@@ -372,12 +338,9 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                     ds_rd128<(2 * m + 1) * 2048>(X[2 * m + 1], rd_next);
                 }
                 if constexpr (!(ABL & 128)) {
-                    constexpr int P2 = FX_V4_DMAPOS == 0 ? 4 : FX_V4_DMAPOS;
-                    constexpr int P3 = FX_V4_DMAPOS == 0 ? 5 : FX_V4_DMAPOS + 4;
-                    constexpr int P4 = FX_V4_DMAPOS == 0 ? 6 : (FX_V4_DMAPOS + 5) % 8;
-                    if constexpr (m == P2) piece(std::integral_constant<int, 2>{}, JP{}, NXT{}, c4, tnext);
-                    if constexpr (m == P3) piece(std::integral_constant<int, 3>{}, JP{}, NXT{}, c4, tnext);
-                    if constexpr (m == P4 && jp == 0) piece(std::integral_constant<int, 4>{}, JP{}, NXT{}, c4, tnext);
+                    if constexpr (m == 4) piece(std::integral_constant<int, 2>{}, JP{}, NXT{}, c4, tnext);
+                    if constexpr (m == 5) piece(std::integral_constant<int, 3>{}, JP{}, NXT{}, c4, tnext);
+                    if constexpr (m == 6 && jp == 0) piece(std::integral_constant<int, 4>{}, JP{}, NXT{}, c4, tnext);
                 }
             });
             if constexpr (HI) {
@@ -420,7 +383,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
 #pragma unroll
         for (int n = 0; n < N; ++n) {
 #pragma unroll
-            for (int m = FX_V4_LATEMIN ? 0 : M - 2; m < M; ++m) gmin[n][m] = min4(acc[m][n]);
+            for (int m = 0; m < M; ++m) gmin[n][m] = min4(acc[m][n]);
             mn[n] = gmin[n][0];
 #pragma unroll
             for (int m = 1; m < M; ++m) mn[n] = __builtin_fminf(mn[n], gmin[n][m]);

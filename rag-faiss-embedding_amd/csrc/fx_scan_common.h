@@ -13,13 +13,8 @@ namespace fx {
 // padding rows (|y|^2 = +inf -> key +inf) never do.
 constexpr float KEY_MAX = FLT_MAX;
 // k_scan_v4's per-query LDS list capacity (KP < LCAP <= 64, one sort64 lane
-// per entry).  56 leaves room for a 6-slot DMA ring (fx_scan.hip FX_V4_NS6);
-// that pair measured 1-2 % slower than 64 entries with 5 slots on (d), (b)
-// and (d) at nq = 256 (profiles/r3/ab/ns6_seed), so 64 is the default
-#ifndef FX_V4_LCAP
-#define FX_V4_LCAP 64
-#endif
-constexpr int LCAP = FX_V4_LCAP;
+// per entry; 56 entries with a 6-slot ring measured 1-2 % slower)
+constexpr int LCAP = 64;
 static_assert(LCAP > KP && LCAP <= 64, "list capacity");
 // global-address-space float: loads through it are global_load (vmcnt only),
 // not flat (which also counts against lgkmcnt as a possible LDS access)

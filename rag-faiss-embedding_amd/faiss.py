@@ -61,6 +61,10 @@ class _FlatIndex:
     """Common implementation of IndexFlatL2 / IndexFlatIP."""
 
     metric_type: int = METRIC_L2
+    _lib = lib  # the ctypes build this index lives in (the diagnostic build: diag.py)
+
+    def _check(self, rc: int) -> None:
+        check(rc, self._lib)
 
     def __init__(self, d: int, dtype: str = "float32", device: int = 0, normalize: bool = False,
                  _handle: Optional[ctypes.c_void_p] = None):
@@ -70,25 +74,26 @@ class _FlatIndex:
         if _handle is not None:
             self._h = _handle
         else:
-            check(lib.fx_index_create(int(d), _DTYPES[dtype], self.metric_type, int(device), ctypes.byref(self._h)))
+            self._check(self._lib.fx_index_create(int(d), _DTYPES[dtype], self.metric_type, int(device),
+                                                  ctypes.byref(self._h)))
         self.device = int(device)
         self.storage_dtype = dtype
         self.is_trained = True
         self.verbose = False
         if normalize:
-            check(lib.fx_index_set_normalize(self._h, 1))
+            self._check(self._lib.fx_index_set_normalize(self._h, 1))
 
     # -- faiss attributes ------------------------------------------------------
     @property
     def d(self) -> int:
         v = ctypes.c_int(0)
-        check(lib.fx_index_dim(self._h, ctypes.byref(v)))
+        self._check(self._lib.fx_index_dim(self._h, ctypes.byref(v)))
         return v.value
 
     @property
     def ntotal(self) -> int:
         v = ctypes.c_int64(0)
-        check(lib.fx_index_ntotal(self._h, ctypes.byref(v)))
+        self._check(self._lib.fx_index_ntotal(self._h, ctypes.byref(v)))
         return v.value
 
     # -- stream plumbing --------------------------------------------------------
@@ -96,9 +101,9 @@ class _FlatIndex:
         if use_torch:
             t = _torch()
             s = t.cuda.current_stream(self.device).cuda_stream
-            check(lib.fx_index_set_stream(self._h, ctypes.c_void_p(s)))
+            self._check(self._lib.fx_index_set_stream(self._h, ctypes.c_void_p(s)))
         else:
-            check(lib.fx_index_set_stream(self._h, None))
+            self._check(self._lib.fx_index_set_stream(self._h, None))
 
     # -- add / search --------------------------------------------------------------
     def add(self, x) -> None:
@@ -108,13 +113,14 @@ class _FlatIndex:
             assert x.device.index == self.device, f"tensor on cuda:{x.device.index}, index on cuda:{self.device}"
             x = x.contiguous()
             self._bind_stream(True)
-            check(lib.fx_index_add(self._h, x.shape[0], ctypes.c_void_p(x.data_ptr()), _tensor_dtype(x),
-                                   _lib.MEM_DEVICE))
+            self._check(self._lib.fx_index_add(self._h, x.shape[0], ctypes.c_void_p(x.data_ptr()),
+                                               _tensor_dtype(x), _lib.MEM_DEVICE))
             return
         x = np.ascontiguousarray(x, dtype=np.float32)
         assert x.ndim == 2 and x.shape[1] == self.d, "dimension mismatch"
         self._bind_stream(False)
-        check(lib.fx_index_add(self._h, x.shape[0], x.ctypes.data_as(ctypes.c_void_p), _lib.F32, _lib.MEM_HOST))
+        self._check(self._lib.fx_index_add(self._h, x.shape[0], x.ctypes.data_as(ctypes.c_void_p), _lib.F32,
+                                           _lib.MEM_HOST))
 
     def search(self, x, k: int, *, D=None, I=None) -> Tuple:
         """``IndexFlat.search`` (faiss_store.py:64): k nearest rows of every
@@ -140,9 +146,9 @@ class _FlatIndex:
                 assert a.dtype == dt and tuple(a.shape) == (nq, k) and a.is_contiguous(), \
                     f"{name} must be a contiguous {dt} tensor of shape ({nq}, {k})"
             self._bind_stream(True)
-            check(lib.fx_index_search(self._h, nq, ctypes.c_void_p(x.data_ptr()), _tensor_dtype(x),
-                                      _lib.MEM_DEVICE, k, ctypes.c_void_p(D.data_ptr()),
-                                      ctypes.c_void_p(I.data_ptr()), _lib.MEM_DEVICE))
+            self._check(self._lib.fx_index_search(self._h, nq, ctypes.c_void_p(x.data_ptr()), _tensor_dtype(x),
+                                                  _lib.MEM_DEVICE, k, ctypes.c_void_p(D.data_ptr()),
+                                                  ctypes.c_void_p(I.data_ptr()), _lib.MEM_DEVICE))
             return D, I
         x = np.ascontiguousarray(x, dtype=np.float32)
         assert x.ndim == 2 and x.shape[1] == self.d, "dimension mismatch"
@@ -155,57 +161,67 @@ class _FlatIndex:
                 a.flags.c_contiguous and a.flags.writeable, \
                 f"{name} must be a writeable C-contiguous {np.dtype(dt).name} array of shape ({nq}, {k})"
         self._bind_stream(False)
-        check(lib.fx_index_search(self._h, nq, x.ctypes.data_as(ctypes.c_void_p), _lib.F32, _lib.MEM_HOST, k,
-                                  Dh.ctypes.data_as(ctypes.c_void_p), Ih.ctypes.data_as(ctypes.c_void_p),
-                                  _lib.MEM_HOST))
+        self._check(self._lib.fx_index_search(self._h, nq, x.ctypes.data_as(ctypes.c_void_p), _lib.F32,
+                                              _lib.MEM_HOST, k, Dh.ctypes.data_as(ctypes.c_void_p),
+                                              Ih.ctypes.data_as(ctypes.c_void_p), _lib.MEM_HOST))
         return Dh, Ih
 
     def last_fallbacks(self) -> int:
         """Queries of the last search whose top-k the scan's candidates could
         not certify (re-scanned with a wide candidate set)."""
         v = ctypes.c_int64(0)
-        check(lib.fx_index_last_fallbacks(self._h, ctypes.byref(v)))
+        self._check(self._lib.fx_index_last_fallbacks(self._h, ctypes.byref(v)))
         return v.value
 
     def last_exact_fallbacks(self) -> int:
         """Of those, the queries the re-scan could not certify either,
         re-ranked by the exact fp64 scan of every row."""
         v = ctypes.c_int64(0)
-        check(lib.fx_index_last_exact_fallbacks(self._h, ctypes.byref(v)))
+        self._check(self._lib.fx_index_last_exact_fallbacks(self._h, ctypes.byref(v)))
+        return v.value
+
+    def last_dropped_candidates(self) -> int:
+        """Candidate entries the last search's exact re-rank dropped for a row
+        id outside [0, ntotal): 0 unless a scan list was corrupted (then the
+        top-k may miss rows; treat it as an error)."""
+        v = ctypes.c_int64(0)
+        self._check(self._lib.fx_index_last_dropped_candidates(self._h, ctypes.byref(v)))
         return v.value
 
     def reset(self) -> None:
-        check(lib.fx_index_reset(self._h))
+        self._check(self._lib.fx_index_reset(self._h))
 
     def reserve(self, n: int) -> None:
-        check(lib.fx_index_reserve(self._h, int(n)))
+        self._check(self._lib.fx_index_reserve(self._h, int(n)))
 
     def reconstruct_n(self, i0: int, n: int) -> np.ndarray:
         out = np.empty((int(n), self.d), dtype=np.float32)
-        check(lib.fx_index_reconstruct_n(self._h, int(i0), int(n), out.ctypes.data_as(ctypes.c_void_p)))
+        self._check(self._lib.fx_index_reconstruct_n(self._h, int(i0), int(n),
+                                                     out.ctypes.data_as(ctypes.c_void_p)))
         return out
 
     def set_id_offset(self, offset: int) -> None:
-        check(lib.fx_index_set_id_offset(self._h, int(offset)))
+        self._check(self._lib.fx_index_set_id_offset(self._h, int(offset)))
 
     def set_option(self, name: str, value: int) -> None:
         """Per-index tuning / diagnostic option (include/fx_index.h
         ``fx_index_set_option``; defaults from the FX_* environment at creation)."""
-        check(lib.fx_index_set_option(self._h, name.encode(), int(value)))
+        self._check(self._lib.fx_index_set_option(self._h, name.encode(), int(value)))
 
     # -- profiling (bench roofline) -------------------------------------------------
     def profile(self, enable: bool = True) -> None:
-        check(lib.fx_index_profile(self._h, 1 if enable else 0))
+        self._check(self._lib.fx_index_profile(self._h, 1 if enable else 0))
 
     def profile_read(self) -> Tuple[float, float, int]:
         a, b, n = ctypes.c_double(0), ctypes.c_double(0), ctypes.c_int64(0)
-        check(lib.fx_index_profile_read(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(n)))
+        self._check(self._lib.fx_index_profile_read(self._h, ctypes.byref(a), ctypes.byref(b),
+                                                    ctypes.byref(n)))
         return a.value, b.value, n.value
 
     def __del__(self):
         h = getattr(self, "_h", None)
         if h is not None and h.value:
-            lib.fx_index_free(h)
+            self._lib.fx_index_free(h)
             self._h = ctypes.c_void_p()
 
 
@@ -224,7 +240,7 @@ class IndexFlatIP(_FlatIndex):
 
 def write_index(index: _FlatIndex, path: str) -> None:
     """``faiss.write_index`` (faiss_store.py:91): IxF2 file, fp32 codes."""
-    check(lib.fx_index_write(index._h, str(path).encode()))
+    check(index._lib.fx_index_write(index._h, str(path).encode()), index._lib)
 
 
 def read_index(path: str, dtype: str = "float32", device: int = 0) -> IndexFlatL2:

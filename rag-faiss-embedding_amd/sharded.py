@@ -8,9 +8,10 @@ fused scan on every rank (local top-k with GLOBAL ids), exchanges the
 collective), and merges them on the device (``fx_merge_shards``).  Because the
 offsets are monotone in rank, "ties -> smaller id" survives the merge.
 
-Works with any ``torch.distributed`` process group: ``nccl`` (= RCCL) with
-device tensors in production, ``gloo`` with host tensors in the CPU tests,
-where ``local_index`` / ``merge_fn`` can be test doubles.
+Works with any ``torch.distributed`` process group: ``nccl`` (= RCCL) in
+production -- host (numpy) queries and results included: the exchange stages
+them on the rank's GPU, RCCL's only memory -- and ``gloo`` with host tensors
+in the CPU tests, where ``local_index`` / ``merge_fn`` can be test doubles.
 """
 from __future__ import annotations
 
@@ -78,26 +79,43 @@ class ShardedIndexFlatL2:
         if b > a:
             self.local.add(x[a - row0:b - row0])
 
-    def search(self, xq, k: int):
-        """Global top-k: local scan -> ONE all_gather of the packed (D, I)
-        lists (nq*k*12 B per rank) -> merge."""
-        D, I = self.local.search(xq, k)
-        if self.world == 1:
-            return D, I
+    def comm_device(self, like: "torch.Tensor") -> "torch.device":
+        """Where the exchange's buffers live.  RCCL (backend ``nccl``) moves
+        device memory only, so host results (the reference's numpy call form,
+        faiss_store.py:61-64) go to this rank's GPU first; gloo takes the
+        tensors where they are."""
+        if dist.get_backend(self.group) == "nccl":
+            return torch.device("cuda", int(getattr(self.local, "device", 0)))
+        return like.device
+
+    def exchange(self, D, I, k: int):
+        """ONE all_gather of the packed local (D, I) lists (nq*k*12 B per
+        rank) -> merge into the global top-k.  Host (numpy) lists come back
+        as numpy, device tensors stay on the device."""
         is_np = isinstance(D, np.ndarray)
-        Dt = torch.from_numpy(D) if is_np else D
-        It = torch.from_numpy(I) if is_np else I
+        Dt = torch.from_numpy(np.ascontiguousarray(D)) if is_np else D
+        It = torch.from_numpy(np.ascontiguousarray(I)) if is_np else I
+        dev = self.comm_device(Dt)
+        Dt, It = Dt.to(dev), It.to(dev)
         nq = Dt.shape[0]
         # pack each (D f32, I i64) entry as 3 int32 words: one collective per batch
-        mine = torch.empty((nq, k, 3), dtype=torch.int32, device=Dt.device)
+        mine = torch.empty((nq, k, 3), dtype=torch.int32, device=dev)
         mine[:, :, 0] = Dt.contiguous().view(torch.int32)
         mine[:, :, 1:] = It.contiguous().view(torch.int32).view(nq, k, 2)
-        allg = torch.empty((self.world * nq, k, 3), dtype=torch.int32, device=Dt.device)
+        allg = torch.empty((self.world * nq, k, 3), dtype=torch.int32, device=dev)
         dist.all_gather_into_tensor(allg, mine, group=self.group)
         allg = allg.view(self.world, nq, k, 3)
         Dg = allg[..., 0].contiguous().view(torch.float32)
         Ig = allg[..., 1:].contiguous().view(torch.int64).view(self.world, nq, k)
         Dm, Im = self._merge(Dg, Ig, k)
         if is_np:
-            return np.asarray(Dm), np.asarray(Im)
+            as_np = lambda t: t.cpu().numpy() if isinstance(t, torch.Tensor) else np.asarray(t)  # noqa: E731
+            return as_np(Dm), as_np(Im)
         return Dm, Im
+
+    def search(self, xq, k: int):
+        """Global top-k: local scan -> exchange (one all_gather + merge)."""
+        D, I = self.local.search(xq, k)
+        if self.world == 1:
+            return D, I
+        return self.exchange(D, I, k)

@@ -20,3 +20,37 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def golden_dir():
     return GOLDEN
+
+
+@pytest.fixture(scope="session")
+def diag_fx():
+    """Indexes bound to the diagnostic build libfx_index_diag.so (the same
+    kernels; test hooks force_fallback / scan_dbg in its option table)."""
+    from rag_faiss_embedding_amd import _lib
+    if _lib.device_count() == 0:
+        pytest.fail("no GPU visible: -m gpu tests must run on the MI355X box")
+    from rag_faiss_embedding_amd import diag
+    return diag
+
+
+@pytest.fixture(autouse=True)
+def _candidate_lists_intact(request, monkeypatch):
+    """In every -m gpu test, every search through the Python API must report
+    0 candidate entries dropped for an out-of-range row id
+    (fx_index_last_dropped_candidates): a corrupted scan list fails the test
+    even when the top-k it left happened to match the oracle."""
+    if request.node.get_closest_marker("gpu") is None:
+        yield
+        return
+    from rag_faiss_embedding_amd import faiss
+    orig = faiss._FlatIndex.search
+    dropped = []
+
+    def search(self, *a, **kw):
+        out = orig(self, *a, **kw)
+        dropped.append(self.last_dropped_candidates())
+        return out
+
+    monkeypatch.setattr(faiss._FlatIndex, "search", search)
+    yield
+    assert not any(dropped), f"searches dropped corrupted candidate ids: {dropped}"

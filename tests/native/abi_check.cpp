@@ -127,6 +127,10 @@ int main() {
     int64_t fb = -1;
     OK(fx_index_last_fallbacks(ix, &fb));
     CHECK(fb >= 0, "fallback count");
+    search_and_check(ix, xb, n, d, 64, 10, rng, "nq=64 k=10 (integrity count)");
+    int64_t dropped = -1;
+    OK(fx_index_last_dropped_candidates(ix, &dropped));
+    CHECK(dropped == 0, "dropped candidate ids %lld", (long long)dropped);
 
     // ---- device queries and results --------------------------------------
     {
@@ -152,6 +156,13 @@ int main() {
     // ---- graph-replayed small host search ---------------------------------
     OK(fx_index_set_option(ix, "search_graph", 1));
     CHECK(fx_index_set_option(ix, "no_such_option", 1) == FX_E_ARG, "unknown option rejected");
+    // range checks; test hooks are not options of the product library
+    CHECK(fx_index_set_option(ix, "search_graph", 2) == FX_E_ARG, "search_graph 2 accepted");
+    CHECK(fx_index_set_option(ix, "union_w", 48) == FX_E_ARG, "union_w 48 accepted");
+    CHECK(fx_index_set_option(ix, "compact_at", 20) == FX_E_ARG, "compact_at 20 accepted");
+    CHECK(fx_index_set_option(ix, "prune_rank", (int64_t)1 << 33) == FX_E_ARG, "prune_rank 2^33 accepted");
+    CHECK(fx_index_set_option(ix, "force_fallback", 1) == FX_E_ARG, "test hook in the product option table");
+    CHECK(fx_index_set_option(ix, "scan_dbg", 32) == FX_E_ARG, "diagnostic switch in the product option table");
     for (int rep = 0; rep < 3; ++rep) search_and_check(ix, xb, n, d, 1, 5, rng, "graph nq=1");
     std::vector<float> extra((size_t)5 * d);
     for (auto& v : extra) v = nd(rng);

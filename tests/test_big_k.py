@@ -101,11 +101,11 @@ def test_k_beyond_ntotal_pads(fx):
 
 
 @pytest.mark.parametrize("k", [10, 100])
-def test_forced_fallback_is_exact(fx, gauss, monkeypatch, k):
+def test_forced_fallback_is_exact(diag_fx, gauss, monkeypatch, k):
     """Every query through the device-gated exact fallback (force_fallback 2:
-    past the re-scan too): same results."""
+    past the re-scan too; a hook of the diagnostic build): same results."""
     xb, xq = gauss
-    ix = fx.IndexFlatL2(384)
+    ix = diag_fx.IndexFlatL2(384)
     ix.add(xb[:100_000])
     ix.set_option("force_fallback", 2)
     D, I = ix.search(xq, k)
@@ -114,13 +114,13 @@ def test_forced_fallback_is_exact(fx, gauss, monkeypatch, k):
     assert_parity(D, I, Dr, Ir)
 
 
-def test_forced_fallback_many_queries(fx, monkeypatch):
+def test_forced_fallback_many_queries(diag_fx, monkeypatch):
     """More flagged queries than the fallback's work-item budget splits for
     (fbs shrinks as nf grows): 5000 flagged queries on a small corpus."""
     rng = np.random.default_rng(6)
     xb = rng.standard_normal((3000, 64)).astype(np.float32)
     xq = rng.standard_normal((5000, 64)).astype(np.float32)
-    ix = fx.IndexFlatL2(64)
+    ix = diag_fx.IndexFlatL2(64)
     ix.add(xb)
     ix.set_option("force_fallback", 2)
     D, I = ix.search(xq, 7)

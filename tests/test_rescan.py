@@ -55,7 +55,7 @@ def test_shell_rescan_certifies(fx, dtype, k):
 
 
 @pytest.mark.parametrize("k", [5, 100])
-def test_forced_levels(fx, k):
+def test_forced_levels(diag_fx, k):
     """force_fallback = 1: every query through the re-scan; = 2: every query
     through the re-scan AND the exact scan.  Results identical and exact."""
     rng = np.random.default_rng(9)
@@ -63,7 +63,7 @@ def test_forced_levels(fx, k):
     xq = rng.standard_normal((300, 128)).astype(np.float32)
     Dr, Ir = C.knn_exact(xq, xb, k)
     for level in (0, 1, 2):
-        ix = fx.IndexFlatL2(128)
+        ix = diag_fx.IndexFlatL2(128)
         ix.add(xb)
         ix.set_option("force_fallback", level)
         D, I = ix.search(xq, k)
@@ -72,14 +72,14 @@ def test_forced_levels(fx, k):
         assert ix.last_exact_fallbacks() == (len(xq) if level == 2 else 0)
 
 
-def test_rescan_device_resident(fx):
+def test_rescan_device_resident(diag_fx):
     """The re-scan is decided on the device: a device-resident search with
     every query forced through it returns exact results stream-ordered."""
     import torch
     rng = np.random.default_rng(10)
     xb = rng.standard_normal((30_000, 256)).astype(np.float32)
     xq = rng.standard_normal((700, 256)).astype(np.float32)
-    ix = fx.IndexFlatL2(256, dtype="bfloat16")
+    ix = diag_fx.IndexFlatL2(256, dtype="bfloat16")
     ix.add(torch.from_numpy(xb).cuda())
     ix.set_option("force_fallback", 1)
     D, I = ix.search(torch.from_numpy(xq).cuda(), 10)

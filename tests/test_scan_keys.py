@@ -21,11 +21,9 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(scope="module")
-def fx():
-    from rag_faiss_embedding_amd import _lib, faiss
-    if _lib.device_count() == 0:
-        pytest.fail("no GPU visible: -m gpu tests must run on the MI355X box")
-    return faiss
+def fx(diag_fx):
+    # the scan's key matrix is dumped by the diagnostic build (FX_SCAN_DBG=32 -> FX_SCAN_KEYS)
+    return diag_fx
 
 
 def _round(a, dtype):

@@ -70,14 +70,14 @@ def test_graph_store_single_queries(fx, monkeypatch):
 
 
 @pytest.mark.parametrize("k", [5, 100])
-def test_graph_replays_the_fallback(fx, monkeypatch, k):
+def test_graph_replays_the_fallback(diag_fx, monkeypatch, k):
     """The captured graph holds the device-gated exact fallback: with every
     query flagged (FX_FORCE_FALLBACK=1) each replay is still exact."""
     monkeypatch.setenv("FX_SEARCH_GRAPH", "1")
     monkeypatch.setenv("FX_FORCE_FALLBACK", "1")
     rng = np.random.default_rng(13)
     xb = rng.standard_normal((8000, 64)).astype(np.float32)
-    ix = fx.IndexFlatL2(64)
+    ix = diag_fx.IndexFlatL2(64)
     ix.add(xb)
     for r in (1, 2, 4000, 7999):
         D, I = ix.search(xb[r:r + 1] + 0.01, k)

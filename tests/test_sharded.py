@@ -8,6 +8,7 @@ import socket
 
 import numpy as np
 import pytest
+import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
@@ -93,3 +94,49 @@ def test_shard_bounds_cover_rows():
             b = [shard_bounds(n, w, r) for r in range(w)]
             assert b[0][0] == 0 and b[-1][1] == n
             assert all(b[i][1] == b[i + 1][0] for i in range(w - 1))
+
+
+class _DevShard(_OracleShard):
+    device = 3  # the rank's GPU ordinal (read by comm_device)
+
+
+def _fake_gather(calls, world):
+    def gather(out, inp, group=None):
+        calls.append(inp.device)
+        # rank r's lists: the same entries with ids shifted by r * 1000
+        parts = []
+        for r in range(world):
+            p = inp.clone()
+            ids = p[:, :, 1:].contiguous().view(torch.int64) + r * 1000
+            p[:, :, 1:] = ids.view(torch.int32).view(p.shape[0], p.shape[1], 2)
+            parts.append(p)
+        out.copy_(torch.cat(parts))
+    return gather
+
+
+
+def test_exchange_buffers_follow_the_backend(monkeypatch):
+    """Under RCCL (backend "nccl") the all_gather must see device tensors even
+    when the local search returned host numpy (the reference's call form,
+    faiss_store.py:61-64); under gloo the host tensors are used as they are.
+    The device decision is comm_device(); the GPU suite runs the real RCCL
+    exchange (test_sharded_gpu.py::test_exchange_under_rccl_host_inputs)."""
+    from rag_faiss_embedding_amd.sharded import ShardedIndexFlatL2
+    monkeypatch.setattr(dist, "is_initialized", lambda: True)
+    monkeypatch.setattr(dist, "get_world_size", lambda g=None: 2)
+    monkeypatch.setattr(dist, "get_rank", lambda g=None: 0)
+    ix = ShardedIndexFlatL2(8, 100, local_index=_DevShard(8, 0), merge_fn=_oracle_merge)
+    host = torch.zeros(2, 2)
+    monkeypatch.setattr(dist, "get_backend", lambda g=None: "nccl")
+    assert ix.comm_device(host) == torch.device("cuda", 3)
+    monkeypatch.setattr(dist, "get_backend", lambda g=None: "gloo")
+    assert ix.comm_device(host) == host.device
+    # the gloo exchange of host lists: numpy in, numpy out, merged across ranks
+    calls = []
+    monkeypatch.setattr(dist, "all_gather_into_tensor", _fake_gather(calls, 2))
+    D = np.array([[0.5, 1.0, 2.0]], dtype=np.float32)
+    I = np.array([[7, 3, 9]], dtype=np.int64)
+    Dm, Im = ix.exchange(D, I, 3)
+    assert calls == [torch.device("cpu")]
+    assert isinstance(Dm, np.ndarray) and isinstance(Im, np.ndarray)
+    assert Im.tolist() == [[7, 1007, 3]] and Dm.tolist() == [[0.5, 0.5, 1.0]]

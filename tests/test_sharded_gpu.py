@@ -73,3 +73,45 @@ def test_sharded_real_index_world2(dtype):
         assert ids_ok and d_ok, (rank, i0)
         lo1 = 40_003 // 2
         assert i0[:3] == sorted(i0[:3]) and {7, lo1 - 1, lo1} <= set(i0[:3]), i0
+
+
+def _rccl_worker(port, q):
+    import torch
+    import amd_fx  # noqa: F401
+    from oracle import cpu as C
+    from rag_faiss_embedding_amd.sharded import ShardedIndexFlatL2
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        rng = np.random.default_rng(5)
+        n, d, k = 20_000, 96, 10
+        xb = rng.standard_normal((n, d)).astype(np.float32)
+        xq = rng.standard_normal((64, d)).astype(np.float32)
+        ix = ShardedIndexFlatL2(d, n, device=0)
+        ix.add(xb)
+        D, I = ix.local.search(xq, k)             # host numpy, as faiss_store.py:61-64
+        assert ix.comm_device(torch.from_numpy(D)) == torch.device("cuda", 0)
+        Dm, Im = ix.exchange(D, I, k)            # real RCCL all_gather + fx_merge_shards
+        Dr, Ir = C.knn_exact(xq, xb, k)
+        q.put((isinstance(Dm, np.ndarray), bool((Im == Ir).all()),
+               bool((np.abs(Dm - Dr) <= 1e-5 * np.maximum(1.0, np.abs(Dr))).all())))
+    except Exception as e:  # noqa: BLE001
+        q.put((False, False, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_exchange_under_rccl_host_inputs():
+    """The exchange step under the nccl (RCCL) backend with the reference's
+    host call form: numpy D / I from the local search are staged on the GPU,
+    gathered by RCCL and merged on the device, and come back as numpy
+    (a world of 1: a one-GPU box cannot host two RCCL ranks)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), q))
+    p.start()
+    res = q.get(timeout=240)
+    p.join(timeout=60)
+    assert res == (True, True, True), res

@@ -262,6 +262,34 @@ def cpu_baseline_and_recall(args, n_total, d, dtype, k, D, I, xq_dev, nthreads, 
     return res
 
 
+def latency_nq1(ix, xq, I_dev, k, calls):
+    """The reference's own call shape (faiss_store.py:61-64,
+    rag_datastore_manager.py:215-218): ONE numpy float32 query in, host D / I
+    out, one search per call, on the same index -- per-call wall latency
+    (H2D, query prep, scan, refine + certification, D2H).  Queries cycle
+    through the bench batch; every call's ids are checked against the
+    device-resident batch result of the same query."""
+    import numpy as np
+    xq_h = xq.float().cpu().numpy()
+    I_ref = I_dev.cpu().numpy()
+    nq = xq_h.shape[0]
+    for q in range(3):  # workspace sizing for nq = 1
+        ix.search(xq_h[q:q + 1], k)
+    ts, same = [], 0
+    for c in range(calls):
+        q = (c * 7919) % nq
+        t0 = time.perf_counter()
+        _, Ih = ix.search(xq_h[q:q + 1], k)
+        ts.append(time.perf_counter() - t0)
+        same += int((Ih[0] == I_ref[q]).all())
+    ts = np.sort(np.asarray(ts)) * 1e3
+    return {"median_ms": round(float(np.median(ts)), 4), "p10_ms": round(float(ts[len(ts) // 10]), 4),
+            "p99_ms": round(float(ts[min(len(ts) - 1, (len(ts) * 99) // 100)]), 4), "calls": calls,
+            "qps_serial": round(1e3 / float(np.median(ts)), 1),
+            "form": "numpy float32 (1, d) query -> host D/I per call (H2D + search + D2H), serial calls",
+            "ids_match_device_path": same == calls}
+
+
 def read_pmc_traffic(cfg_name, n_local, nq, data="synthetic"):
     """HBM bytes per scan launch from a committed rocprofv3 --pmc summary of
     this same workload (profiles/pmc_scan_<cfg>[_clustered].json), or None."""
@@ -297,6 +325,7 @@ def main():
     ap.add_argument("--cpu-queries", type=int, default=0, help="fixed CPU sample (0: auto-size)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="target CPU baseline sample time")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline / recall leg")
+    ap.add_argument("--latency-calls", type=int, default=200, help="single-query host calls of the latency_nq1 leg")
     ap.add_argument("--ranks-check", action="store_true", help=argparse.SUPPRESS)  # tests: report the rank, exit
     args = ap.parse_args()
 
@@ -364,11 +393,17 @@ def main():
         exact_fb = ix.last_exact_fallbacks()
     except AttributeError:  # an older library under FX_INDEX_LIB (same-box A/B)
         exact_fb = None
+    try:  # candidate-list integrity: ids outside [0, ntotal) the refine had to drop (0 unless broken)
+        dropped = ix.last_dropped_candidates()
+    except AttributeError:
+        dropped = None
     if world > 1:
-        t = torch.tensor([elapsed, scan_ms / max(launches, 1), float(fallbacks)], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed, scan_ms / max(launches, 1), float(fallbacks), float(dropped or 0)],
+                         dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, scan_avg_ms = float(t[0].item()), float(t[1].item())
         fallbacks = int(t[2].item())
+        dropped = None if dropped is None else int(t[3].item())
     else:
         scan_avg_ms = scan_ms / max(launches, 1)
 
@@ -426,6 +461,7 @@ def main():
         },
         "fallback_queries_last_step": fallbacks,
         "exact_fallback_queries_last_step": exact_fb,
+        "dropped_candidate_ids_last_step": dropped,
         "roofline": roof,
     }
     if world == 1:
@@ -446,6 +482,10 @@ def main():
             }
         except Exception as e:  # noqa: BLE001 -- a side measurement never breaks the bench line
             log("pcie-inclusive leg failed:", e)
+        try:
+            out["latency_nq1"] = latency_nq1(ix, xq, I, k, args.latency_calls)
+        except Exception as e:  # noqa: BLE001
+            log("latency_nq1 leg failed:", e)
     if rank == 0 and not args.no_cpu:
         nthreads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
         extra = cpu_baseline_and_recall(args, n_total, d, dtype, k, D, I, xq, nthreads, device)

@@ -51,10 +51,9 @@ constexpr int S_NSLOT_B = 4 * 256;              // [wave][32 row norms | 32 thre
 constexpr int S_RING_OFF = S_NORM_OFF + 4 * S_NSLOT_B;
 template <int NS>
 struct ScanLds {
-    static constexpr int LD_OFF = S_RING_OFF + NS * S_STAGE;
-    static constexpr int LI_OFF = LD_OFF + TILE_Q * LCAP * 4;
-    static constexpr int TRASH_OFF = LI_OFF + TILE_Q * LCAP * 4;  // [4 waves][64 lanes] sink of the branch-free push
-    static constexpr int BYTES = TRASH_OFF + 4 * 256;
+    static constexpr int LST_OFF = S_RING_OFF + NS * S_STAGE;  // [128 queries][LCAP] (key, row) entries
+    static constexpr int UNION_OFF = LST_OFF + TILE_Q * LCAP * 8;  // [4 waves][2 slots][256 keys] (compact_regs)
+    static constexpr int BYTES = UNION_OFF + 4 * 2 * 1024;
     static_assert(BYTES <= 160 * 1024, "LDS budget");
 };
 
@@ -105,11 +104,11 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
     const int64_t q0 = (int64_t)qtile * TILE_Q;
     if (p.trace && tid == 0) trace_block_start(p, qtile, split);
 
-    float* lst_d = (float*)(smem + LDS::LD_OFF);
-    int* lst_i = (int*)(smem + LDS::LI_OFF);
+    uint2* lst = (uint2*)(smem + LDS::LST_OFF);
     const int qw0 = wave * 32;  // this wave's queries (tile-local)
-    const uint32_t ld_off = lds_off(lst_d), li_off = lds_off(lst_i);
-    const uint32_t trash = lds_off(smem + LDS::TRASH_OFF) + (uint32_t)(wave * 256 + lane * 4);
+    const uint32_t lst_off = lds_off(lst);
+    const uint32_t ulds = lds_off(smem + LDS::UNION_OFF) + (uint32_t)(wave * 2048);
+    int upq[2] = {-1, -1};  // deferred union bounds in flight (compact_regs / union_finish)
     // list counts and thresholds of this lane's two queries (compact_regs)
     ListRegs lr;
     lr.cnt[0] = lr.cnt[1] = 0;
@@ -191,8 +190,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
     for (int n = 0; n < N; ++n) qloc[n] = qw0 + n * 16 + (lane & 15);
     const bool qv0 = q0 + qloc[0] < nq, qv1 = q0 + qloc[1] < nq;
     // per-lane LDS addresses: my two queries' list rows, my thresholds in a norm slot
-    const uint32_t lq[N] = {ld_off + (uint32_t)(qloc[0] * LCAP * 4), ld_off + (uint32_t)(qloc[1] * LCAP * 4)};
-    const uint32_t li_d = li_off - ld_off;
+    const uint32_t lq[N] = {lst_off + (uint32_t)(qloc[0] * LCAP * 8), lst_off + (uint32_t)(qloc[1] * LCAP * 8)};
     const uint32_t gt_lane = (uint32_t)(128 + (lane & 15) * 4);
     const uint32_t nrm_lane = (uint32_t)(rl0 * 4);
 
@@ -389,6 +387,9 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
             for (int m = 1; m < M; ++m) mn[n] = __builtin_fminf(mn[n], gmin[n][m]);
         }
         if constexpr (ABL & 64) stq[12] += __builtin_amdgcn_s_memtime() - s_end;  // fast epilogue
+        // union bounds of the last tile's compactions (their windows have landed)
+        if (__builtin_expect(upq[0] >= 0 || upq[1] >= 0, 0))
+            union_finish(upq, ulds, lr, gtq, p.splits, split, p.prune_rank, p.union_w, lane);
         // unlikely: the slow path's code (pushes, compaction) is laid out
         // after the loop, so the hot path runs through without a jump over it
         // (the loop body then fits the instruction cache)
@@ -410,8 +411,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                     static_for<M>([&](auto MM) {
                         constexpr int m = decltype(MM)::value;
                         if (__builtin_amdgcn_ballot_w64(gmin[n][m] <= tn[n])) {
-                            ovf |= push_reg<M, N>(acc, n, m, 15u, tn[n], trow0 + rl0 + m * 16, rlim, lq[n], li_d, trash,
-                                                  lr.cnt[n], lane, pend[n]);
+                            ovf |= push_col<M, N>(acc, n, m, 15u, tn[n], trow0 + rl0 + m * 16, rlim, lq[n], lr.cnt[n],
+                                                  lane, pend[n]);
                             if constexpr (ABL & (64 | 1024)) stq[10] += 1;
                         }
                     });
@@ -424,8 +425,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
             while (__builtin_amdgcn_ballot_w64(need)) {
                 uint64_t s_cp = 0;
                 if constexpr (ABL & (64 | 1024)) s_cp = __builtin_amdgcn_s_memtime();
-                lr = compact_regs(lst_d, lst_i, lr, p.share ? gtq : nullptr, qw0, lane, p.pub ? pubw : nullptr, p.splits,
-                                  split, p.prune_rank, cat, p.union_w);
+                lr = compact_regs(lst, lr, p.share ? gtq : nullptr, qw0, lane, p.pub ? pubw : nullptr, p.splits,
+                                  split, p.prune_rank, cat, p.union_w, upq, ulds);
                 if constexpr (ABL & (64 | 1024)) {
                     stq[8] += 1;
                     stq[9] += __builtin_amdgcn_s_memtime() - s_cp;
@@ -440,8 +441,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                         constexpr int m = decltype(MM)::value;
                         const unsigned el = (pn >> (4 * m)) & 15u;
                         if (__builtin_amdgcn_ballot_w64(el != 0u))
-                            ovf |= push_reg<M, N>(acc, n, m, el, tq, trow0 + rl0 + m * 16, rlim, lq[n], li_d, trash,
-                                                  lr.cnt[n], lane, pend[n]);
+                            ovf |= push_col<M, N>(acc, n, m, el, tq, trow0 + rl0 + m * 16, rlim, lq[n], lr.cnt[n],
+                                                  lane, pend[n]);
                     });
                 });
                 need = ovf;
@@ -476,8 +477,9 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
         if (q0 + q >= nq) break;
         const int cq = qi < 16 ? __builtin_amdgcn_readlane(lr.cnt[0], qi) : __builtin_amdgcn_readlane(lr.cnt[1], qi - 16);
         const int cn = min(cq, LCAP);
-        float d = lane < cn ? lst_d[q * LCAP + lane] : FX_INF;
-        int i = lane < cn ? lst_i[q * LCAP + lane] : INT_MAX;
+        const uint2 e = lane < cn ? lst[q * LCAP + lane] : make_uint2(__float_as_uint(FX_INF), (unsigned)INT_MAX);
+        float d = __uint_as_float(e.x);
+        int i = (int)e.y;
         sort64(d, i, lane);
         if (lane < KP) {
             p.cand_d[(obase + q) * KP + lane] = d;
@@ -532,6 +534,14 @@ static hipError_t scan_v4_t(const ScanParams& p, hipStream_t s) {
 template <int DT, int METRIC>
 static hipError_t scan_rows(const ScanParams& p, hipStream_t s, bool* handled) {
     *handled = true;
+#ifdef FX_SCAN_DEV  // kernel-development build (Makefile `dev`): 1536-B rows, bf16 / split fp32, L2 only
+    if constexpr (METRIC == L2 && (DT == BF16 || DT == F32S)) {
+        if (p.row_bytes == 1536)
+            return p.nq_dev ? scan_v4_t<DT, METRIC, 24, RESCAN>(p, s) : scan_v4_t<DT, METRIC, 24>(p, s);
+    }
+    *handled = false;
+    return hipSuccess;
+#else
     switch (p.row_bytes / 64) {
         // the re-scan of uncertified queries (p.nq_dev set) runs the same code
         // under its own kernel name (ABL bit RESCAN changes nothing else), so
@@ -542,6 +552,7 @@ static hipError_t scan_rows(const ScanParams& p, hipStream_t s, bool* handled) {
         case 24: return p.nq_dev ? scan_v4_t<DT, METRIC, 24, RESCAN>(p, s) : scan_v4_t<DT, METRIC, 24>(p, s);
         default: *handled = false; return hipSuccess;
     }
+#endif
 }
 
 hipError_t launch_scan_mfma(int st_dt, int metric, const ScanParams& p, hipStream_t s, bool* handled) {

@@ -95,6 +95,7 @@ struct Options {
     int prune_rank = 0;      // FX_PRUNE_RANK: rank of the shared threshold (0: max(6k/5, 12))
     int compact_at = 0;      // FX_COMPACT_AT: list fill that triggers a compaction (0: default, KP < v <= CAP)
     int union_w = 0;         // FX_UNION_W: splits per union-bound window (16, 32, 64; 0: by split count)
+    int union_defer = 1;     // FX_UNION_DEFER: union bounds fetched by LDS-DMA, bounded a tile later
     int graph_verbose = 0;   // FX_SEARCH_GRAPH_VERBOSE
 #ifdef FX_DIAG
     int force_fallback = 0;  // FX_FORCE_FALLBACK: flag every query (1: -> re-scan, 2: -> exact scan)
@@ -121,6 +122,7 @@ struct Options {
         num("FX_PRUNE_RANK", prune_rank);
         num("FX_COMPACT_AT", compact_at);
         num("FX_UNION_W", union_w);
+        num("FX_UNION_DEFER", union_defer);
         num("FX_SEARCH_GRAPH_VERBOSE", graph_verbose);
         (void)str;
 #ifdef FX_DIAG
@@ -154,6 +156,7 @@ struct Options {
             {"prune_rank", &prune_rank, 0, KP, nullptr, 0},
             {"compact_at", &compact_at, 0, CAP, nullptr, 0},
             {"union_w", &union_w, 0, 64, kWindows, 4},
+            {"union_defer", &union_defer, 0, 1, nullptr, 0},
 #ifdef FX_DIAG
             {"force_fallback", &force_fallback, 0, 2, nullptr, 0},
             {"scan_dbg", &scan_dbg, 0, 1 << 20, nullptr, 0},
@@ -319,6 +322,7 @@ void plan_scan(const FxIndex* h, int64_t nq, int k, ScanParams& p) {
     p.compact_at = h->opt.compact_at > KP && h->opt.compact_at <= CAP ? h->opt.compact_at : CAP;
     p.share = k <= KP ? 1 : 0;
     p.union_w = 16;
+    p.union_defer = h->opt.union_defer;
     const int ntl = p.n_qtiles, nct = p.n_ctiles;
     constexpr int min_tiles = 4;
     // placement (map_tile): corpus-partitioned by default (config (d): 257 vs
@@ -680,7 +684,7 @@ hipError_t enqueue_search(FxIndex* h, SearchPlan& P, hipStream_t s, bool timed, 
     if ((P.sp.dbg & ~32) != 0) return hipSuccess;  // ablated scans: results invalid, no fallback chain
 #endif
     if ((e = launch_prep_queries(P.pp2, s)) != hipSuccess) return e;
-    if ((e = hipMemsetD32Async((hipDeviceptr_t)P.sp2.gtau, 0xff800000u, (size_t)P.nq_pad, s)) != hipSuccess)
+    if ((e = hipMemsetD32Async((hipDeviceptr_t)P.sp2.gtau, 0xff800000u, (size_t)P.pp2.nq_pad, s)) != hipSuccess)
         return e;
     if ((e = launch_scan(P.scan_dt, h->metric, P.sp2, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(P.n_exact, 0, 4, s)) != hipSuccess) return e;
@@ -861,6 +865,7 @@ std::vector<uint64_t> graph_key(const FxIndex* h, int64_t nq, int q_dtype, int k
             (uint64_t)h->img_kind, (uint64_t)h->centred, (uint64_t)h->img_rows,
             (uint64_t)o.force_fallback, (uint64_t)o.place, (uint64_t)o.sx, (uint64_t)o.reduce_cand,
             (uint64_t)o.pub, (uint64_t)o.prune_rank, (uint64_t)o.compact_at, (uint64_t)o.union_w,
+            (uint64_t)o.union_defer,
             (uint64_t)(uintptr_t)h->codes, (uint64_t)(uintptr_t)h->norms, (uint64_t)(uintptr_t)h->split.p,
             (uint64_t)(uintptr_t)h->cnorms.p, (uint64_t)(uintptr_t)h->centre.p, (uint64_t)(uintptr_t)h->qshift.p,
             (uint64_t)(uintptr_t)h->qin.p, (uint64_t)(uintptr_t)h->qf32.p, (uint64_t)(uintptr_t)h->qop.p,

@@ -73,6 +73,8 @@ struct ScanParams {
                                 // [grid][4 waves][16] per-wave cycle sums of the scan's phases
     const int* nq_dev;          // non-null (the re-scan of uncertified queries): the live query
                                 // count is min(*nq_dev, nq), known only on the device
+    int union_defer;            // 1: a compaction's union bound is fetched by LDS-DMA and bounded at
+                                // the next tile's epilogue (compact_regs); 0: waited for in place
 };
 
 // queries are zero-padded to a multiple of QPAD (the scan's query tile)

@@ -234,7 +234,7 @@ __device__ __forceinline__ void union_finish(int (&upq)[2], uint32_t ulds, const
 }
 __device__ __forceinline__ ListRegs compact_regs(uint2* lst, ListRegs r, unsigned* gtq, int qw0, int lane,
                                               float* pub, int splits, int split, int rank, int at, int uw,
-                                              int (&upq)[2], uint32_t ulds) {
+                                              int (&upq)[2], uint32_t ulds, int defer) {
     int (&cntv)[2] = r.cnt;
     float (&tauv)[2] = r.tau;
     const uint64_t f0 = __builtin_amdgcn_ballot_w64(lane < 16 && cntv[0] >= at);
@@ -279,7 +279,7 @@ __device__ __forceinline__ ListRegs compact_regs(uint2* lst, ListRegs r, unsigne
     // deferred: up to two windows fetched into the union slots (union_finish)
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-        if (rest == 0 || upq[u] >= 0) continue;
+        if (rest == 0 || upq[u] >= 0 || !defer) continue;
         const int qi = __builtin_ctzll(rest);
         rest &= rest - 1;
         const int l = lane >> (le - 2), e4 = lane & ((1 << (le - 2)) - 1);

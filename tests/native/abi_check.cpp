@@ -128,6 +128,9 @@ int main() {
     OK(fx_index_last_fallbacks(ix, &fb));
     CHECK(fb >= 0, "fallback count");
     search_and_check(ix, xb, n, d, 64, 10, rng, "nq=64 k=10 (integrity count)");
+    // a batch above the re-scan's capacity (RESCAN_MAX = 2048 queries): its
+    // workspace stays capped, the batch still runs whole
+    search_and_check(ix, xb, n, d, 2100, 10, rng, "nq=2100 k=10 (re-scan capacity)");
     int64_t dropped = -1;
     OK(fx_index_last_dropped_candidates(ix, &dropped));
     CHECK(dropped == 0, "dropped candidate ids %lld", (long long)dropped);

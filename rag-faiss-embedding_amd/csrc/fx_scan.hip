@@ -166,6 +166,18 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
             dma_norm_piece(decltype(NXT)::value ? nv_nxt : nv_cur, nslot_w + (uint32_t)(tnext & 3) * S_NSLOT_B);
     };
 
+    // a corpus piece fused with the MFMA pair before it (AsmMmaV::mma2_dma:
+    // the pair is the M0-write -> LDS-DMA wait state instead of an s_nop)
+    constexpr bool FUSE = LN == 1 && DT != F32 && !(ABL & (2 | 4 | 128));
+    auto mma_piece = [&](auto INITC, auto W, auto JP, auto NXT, uint32_t slot, f32x4& c0, f32x4& c1,
+                         const frag_t& a, const bfrag_t& b0, const bfrag_t& b1, const f32x4& ci) {
+        constexpr int init = decltype(INITC)::value, w = decltype(W)::value, jp = decltype(JP)::value;
+        static_assert(w < 4, "corpus pieces only");
+        const char* cb = decltype(NXT)::value ? cb_nxt : cb_cur;
+        const uint32_t m0 = m0w + slot * S_STAGE + w * 1024;
+        AsmMmaV<DT>::template mma2_dma<init, jp * STAGE_B>(c0, c1, a, b0, b1, ci, voffA, cb + w * 8 * RB, m0);
+    };
+
     // prologue: stages 0 .. NS-2 (all in tile 0: SPT >= NS - 1)
     static_for<NS - 1>([&](auto ST) {
         constexpr int st = decltype(ST)::value;
@@ -271,7 +283,11 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
             static_for<M>([&](auto MM) {
                 constexpr int m = decltype(MM)::value;
                 constexpr int INIT = j == 0 ? (METRIC == L2 ? 1 : 2) : 0;
-                if constexpr (!(ABL & 4))
+                constexpr bool FP = FUSE && (m == 4 || m == 6);  // pair m carries corpus piece m / 2 - 2
+                if constexpr (FP)
+                    mma_piece(std::integral_constant<int, INIT>{}, std::integral_constant<int, m / 2 - 2>{}, JP{},
+                              NXT{}, c4, acc[m][0], acc[m][1], X[m], b[kq0][0], b[kq0][1], yin[m]);
+                else if constexpr (!(ABL & 4))
                     AsmMmaV<DT>::template mma2<INIT>(acc[m][0], acc[m][1], X[m], b[kq0][0], b[kq0][1], yin[m]);
                 // half 1 of this stage: two reads per pair over the first four
                 // pairs, so the mid-stage wait finds them landed
@@ -292,7 +308,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                         static_for<4>([&](auto W) { piece(W, JP{}, NXT{}, c4, tnext); });
                         if constexpr (jp == 0) piece(std::integral_constant<int, 4>{}, JP{}, NXT{}, c4, tnext);
                     }
-                } else {  // a stage's corpus pieces after MFMA pairs 4, 6 (half 0) and 4, 5 (half 1)
+                } else if constexpr (!FP) {  // a stage's corpus pieces after MFMA pairs 4, 6 (half 0) and 4, 5 (half 1)
                     if constexpr (m == 4) piece(std::integral_constant<int, 0>{}, JP{}, NXT{}, c4, tnext);
                     if constexpr (m == 6) piece(std::integral_constant<int, 1>{}, JP{}, NXT{}, c4, tnext);
                 }
@@ -327,7 +343,11 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
             const uint32_t rd_next = lds_base + S_RING_OFF + c1 * S_STAGE + rd_lane;
             static_for<M>([&](auto MM) {
                 constexpr int m = decltype(MM)::value;
-                if constexpr (!(ABL & 4))
+                constexpr bool FP = FUSE && (m == 4 || m == 5);  // pair m carries corpus piece m - 2
+                if constexpr (FP)
+                    mma_piece(std::integral_constant<int, 0>{}, std::integral_constant<int, m - 2>{}, JP{}, NXT{}, c4,
+                              acc[m][0], acc[m][1], Y[m], b[kq0 + 1][0], b[kq0 + 1][1], yin[m]);
+                else if constexpr (!(ABL & 4))
                     AsmMmaV<DT>::template mma2<0>(acc[m][0], acc[m][1], Y[m], b[kq0 + 1][0], b[kq0 + 1][1], yin[m]);
                 // half 0 of stage g+1: two reads per pair over the first four
                 // pairs (X[2m+1]'s last reader is >= 8 MFMAs back)
@@ -336,8 +356,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                     ds_rd128<(2 * m + 1) * 2048>(X[2 * m + 1], rd_next);
                 }
                 if constexpr (!(ABL & 128)) {
-                    if constexpr (m == 4) piece(std::integral_constant<int, 2>{}, JP{}, NXT{}, c4, tnext);
-                    if constexpr (m == 5) piece(std::integral_constant<int, 3>{}, JP{}, NXT{}, c4, tnext);
+                    if constexpr (m == 4 && !FP) piece(std::integral_constant<int, 2>{}, JP{}, NXT{}, c4, tnext);
+                    if constexpr (m == 5 && !FP) piece(std::integral_constant<int, 3>{}, JP{}, NXT{}, c4, tnext);
                     if constexpr (m == 6 && jp == 0) piece(std::integral_constant<int, 4>{}, JP{}, NXT{}, c4, tnext);
                 }
             });

@@ -379,8 +379,17 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
         });
 
         // ---- epilogue of tile t: the accumulator holds the keys ------------
-        acc_fence_v(acc);
+        // Group minima first, group by group (asm volatile: in this order):
+        // acc[0..5] take 24 VALU instructions, so the last pairs' XDL writes
+        // (acc[6], acc[7]) are >= 24 wait states old when read -- past the 11
+        // (8-pass) / 19 (16-pass) states of the XDL-write -> VALU-read hazard,
+        // with no s_nop pad (acc_fence_v: ~80 cycles per tile)
+#pragma unroll
+        for (int m = 0; m < M; ++m)
+#pragma unroll
+            for (int n = 0; n < N; ++n) gmin[n][m] = min4(acc[m][n]);
         if (__builtin_expect(p.dbgbuf != nullptr, 0)) {  // diagnostics (FX_SCAN_DBG & 32): every key -> [nq_pad][cap rows]
+            acc_fence_v(acc);
             float* keys = (float*)p.dbgbuf;
             const int64_t ld = (int64_t)p.n_ctiles * TILE_R;
 #pragma unroll
@@ -400,8 +409,6 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
         float mn[N];
 #pragma unroll
         for (int n = 0; n < N; ++n) {
-#pragma unroll
-            for (int m = 0; m < M; ++m) gmin[n][m] = min4(acc[m][n]);
             mn[n] = gmin[n][0];
 #pragma unroll
             for (int m = 1; m < M; ++m) mn[n] = __builtin_fminf(mn[n], gmin[n][m]);

@@ -331,10 +331,14 @@ __device__ __forceinline__ ListRegs compact_regs(uint2* lst, ListRegs r, unsigne
 // canonicalise every operand first).  volatile: it stays where it is placed
 // among the asm MFMAs (the caller keeps >= 2 MFMA pairs between the last XDL
 // write of `a` and this read; hipcc does not see the asm MFMAs' hazards)
+// One asm block: the compiler pads an s_nop between two inline-asm blocks
+// where the second reads what the first wrote (it cannot see inside them);
+// inside one block the VALU -> VALU read needs no wait state.
 __device__ __forceinline__ float min4(const f32x4& a) {
-    float t, r;
-    asm volatile("v_min_f32 %0, %1, %2" : "=v"(t) : "v"(a[2]), "v"(a[3]));
-    asm volatile("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a[0]), "v"(a[1]), "v"(t));
+    float r;
+    asm volatile("v_min3_f32 %0, %1, %2, %3\n\tv_min_f32 %0, %0, %4"
+                 : "=&v"(r)
+                 : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]));
     return r;
 }
 

@@ -8,7 +8,7 @@
 set -euo pipefail
 t=$1; o=gpurun_out/$t; mkdir -p $o
 L=rag-faiss-embedding_amd
-tools/r4_ab.sh ${t}ab "$L/libfx_index_r3.so|-" "$L/libfx_index_r4b.so|FX_UNION_DEFER=0" "$L/libfx_index_r4b.so|-" "$L/libfx_index.so|-"
+tools/r4_ab.sh ${t}ab "$L/libfx_index_r3.so|-" "$L/libfx_index_r4b.so|-" "$L/libfx_index_r4f.so|-" "$L/libfx_index.so|-"
 timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $o/pytest.log 2>&1
 tail -3 $o/pytest.log
 echo check done

@@ -51,9 +51,13 @@ constexpr int S_NSLOT_B = 4 * 256;              // [wave][32 row norms | 32 thre
 constexpr int S_RING_OFF = S_NORM_OFF + 4 * S_NSLOT_B;
 template <int NS>
 struct ScanLds {
-    static constexpr int LST_OFF = S_RING_OFF + NS * S_STAGE;  // [128 queries][LCAP] (key, row) entries
-    static constexpr int UNION_OFF = LST_OFF + TILE_Q * LCAP * 8;  // [4 waves][2 slots][256 keys] (compact_regs)
-    static constexpr int BYTES = UNION_OFF + 4 * 2 * 1024;
+    // LDS-DMA destinations (norm slots, ring, union slots) first: an LDS-DMA
+    // reaches only the first 128 KiB through M0 (measured: union slots placed
+    // at 148 KiB read back garbage); the lists are written by ds_write
+    static constexpr int UNION_OFF = S_RING_OFF + NS * S_STAGE;    // [4 waves][2 slots][256 keys] (compact_regs)
+    static constexpr int LST_OFF = UNION_OFF + 4 * 2 * 1024;      // [128 queries][LCAP] (key, row) entries
+    static constexpr int BYTES = LST_OFF + TILE_Q * LCAP * 8;
+    static_assert(LST_OFF <= 128 * 1024, "every LDS-DMA destination below 128 KiB");
     static_assert(BYTES <= 160 * 1024, "LDS budget");
 };
 

@@ -401,16 +401,6 @@ struct Bf32 { float x[4]; };
 // operand registers live and pinned, see fx_scan.hip) and acc_fence_v pads
 // the XDL-write -> VALU-read wait states before an epilogue reads them.
 template <int DT> struct AsmMmaV;
-// One MFMA pair followed by one LDS-DMA piece in a single asm block (16-bit
-// operands): M0 is written before the pair, so the two MFMAs are the
-// M0-write -> LDS-DMA wait state the separate form pays an s_nop for
-// (dma_piece, fx_scan_common.h).  C0 / C1: the two MFMAs' srcC operand text.
-#define FX_MMA2_DMA(OP, C0, C1)                                                                        \
-    asm volatile(OP " %0, %2, %3, " C0 "\n\t" OP " %1, %2, %4, " C1 "\n\t"                          \
-                    "global_load_lds_dwordx4 %6, %7 offset:%8"                                        \
-                 : "+v"(c0), "+v"(c1)                                                                 \
-                 : "v"(a), "a"(b0), "a"(b1), "v"(ci), "v"(voff), "s"(sbase), "i"(OFF), "{m0}"(lds - OFF) \
-                 : "memory")
 template <> struct AsmMmaV<BF16> {
     typedef bf16x8 A;
     typedef bf16x8 B;
@@ -431,15 +421,6 @@ template <> struct AsmMmaV<BF16> {
                          "v_mfma_f32_16x16x32_bf16 %1, %2, %4, 0"
                          : "+v"(c0), "+v"(c1) : "v"(a), "a"(b0), "a"(b1));
         }
-    }
-    // mma2 then the LDS-DMA piece (voff + sbase + OFF -> LDS lds + 16 lane)
-    template <int INIT, int OFF>
-    static __device__ __forceinline__ void mma2_dma(f32x4& c0, f32x4& c1, const A& a, const B& b0, const B& b1,
-                                                    const f32x4& ci, uint32_t voff, const char* sbase, uint32_t lds) {
-        static_assert(OFF >= 0 && OFF < 4096, "M0 = lds - OFF must not wrap");
-        if constexpr (INIT == 0) FX_MMA2_DMA("v_mfma_f32_16x16x32_bf16", "%0", "%1");
-        else if constexpr (INIT == 1) FX_MMA2_DMA("v_mfma_f32_16x16x32_bf16", "%5", "%5");
-        else FX_MMA2_DMA("v_mfma_f32_16x16x32_bf16", "0", "0");
     }
 };
 template <> struct AsmMmaV<F16> {
@@ -462,14 +443,6 @@ template <> struct AsmMmaV<F16> {
                          "v_mfma_f32_16x16x32_f16 %1, %2, %4, 0"
                          : "+v"(c0), "+v"(c1) : "v"(a), "a"(b0), "a"(b1));
         }
-    }
-    template <int INIT, int OFF>
-    static __device__ __forceinline__ void mma2_dma(f32x4& c0, f32x4& c1, const A& a, const B& b0, const B& b1,
-                                                    const f32x4& ci, uint32_t voff, const char* sbase, uint32_t lds) {
-        static_assert(OFF >= 0 && OFF < 4096, "M0 = lds - OFF must not wrap");
-        if constexpr (INIT == 0) FX_MMA2_DMA("v_mfma_f32_16x16x32_f16", "%0", "%1");
-        else if constexpr (INIT == 1) FX_MMA2_DMA("v_mfma_f32_16x16x32_f16", "%5", "%5");
-        else FX_MMA2_DMA("v_mfma_f32_16x16x32_f16", "0", "0");
     }
 };
 // F32S (split fp32) runs on the bf16 pipe; the scan issues the extra products
@@ -509,12 +482,6 @@ template <> struct AsmMmaV<F32> {
         }
 #undef FX_F32_TAIL
 #undef FX_F32_OPS
-    }
-    // no fused form: the fp32 pair is 8 MFMAs (k_scan_v4 issues its pieces separately)
-    template <int INIT, int OFF>
-    static __device__ __forceinline__ void mma2_dma(f32x4&, f32x4&, const A&, const B&, const B&, const f32x4&,
-                                                    uint32_t, const char*, uint32_t) {
-        static_assert(INIT < 0, "k_scan_v4 does not fuse corpus pieces into fp32 MFMA pairs");
     }
 };
 

@@ -40,7 +40,8 @@ namespace fx {
 // DMA ring slots (NS - 1 stages in flight).  Measured: a
 // 6-slot ring (with 56-entry lists to fit the LDS), counted per-pair LDS
 // waits instead of the mid-stage lgkmcnt(0), group minima beside the last
-// MFMAs and other DMA issue points were all no faster
+// MFMAs, other DMA issue points and corpus pieces fused into the MFMA pair
+// before them were all no faster
 template <int KSTEPS>
 constexpr int ring_slots() { return 5; }
 constexpr int S_STAGE = TILE_R * STAGE_B;       // 16 KiB = 128 rows x 128 B
@@ -51,13 +52,12 @@ constexpr int S_NSLOT_B = 4 * 256;              // [wave][32 row norms | 32 thre
 constexpr int S_RING_OFF = S_NORM_OFF + 4 * S_NSLOT_B;
 template <int NS>
 struct ScanLds {
-    // LDS-DMA destinations (norm slots, ring, union slots) first: an LDS-DMA
-    // reaches only the first 128 KiB through M0 (measured: union slots placed
-    // at 148 KiB read back garbage); the lists are written by ds_write
-    static constexpr int UNION_OFF = S_RING_OFF + NS * S_STAGE;    // [4 waves][2 slots][256 keys] (compact_regs)
-    static constexpr int LST_OFF = UNION_OFF + 4 * 2 * 1024;      // [128 queries][LCAP] (key, row) entries
-    static constexpr int BYTES = LST_OFF + TILE_Q * LCAP * 8;
-    static_assert(LST_OFF <= 128 * 1024, "every LDS-DMA destination below 128 KiB");
+    // LDS-DMA destinations first (norm slots, ring, union slots), then the lists
+    static constexpr int UNION_OFF = S_RING_OFF + NS * S_STAGE;  // [4 waves][2 slots][256 keys] (compact_regs)
+    static constexpr int LD_OFF = UNION_OFF + 4 * 2 * 1024;
+    static constexpr int LI_OFF = LD_OFF + TILE_Q * LCAP * 4;
+    static constexpr int TRASH_OFF = LI_OFF + TILE_Q * LCAP * 4;  // [4 waves][64 lanes] sink of the branch-free push
+    static constexpr int BYTES = TRASH_OFF + 4 * 256;
     static_assert(BYTES <= 160 * 1024, "LDS budget");
 };
 
@@ -108,10 +108,12 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
     const int64_t q0 = (int64_t)qtile * TILE_Q;
     if (p.trace && tid == 0) trace_block_start(p, qtile, split);
 
-    uint2* lst = (uint2*)(smem + LDS::LST_OFF);
+    float* lst_d = (float*)(smem + LDS::LD_OFF);
+    int* lst_i = (int*)(smem + LDS::LI_OFF);
     const int qw0 = wave * 32;  // this wave's queries (tile-local)
-    const uint32_t lst_off = lds_off(lst);
-    const uint32_t ulds = lds_off(smem + LDS::UNION_OFF) + (uint32_t)(wave * 2048);
+    const uint32_t ld_off = lds_off(lst_d), li_off = lds_off(lst_i);
+    const uint32_t trash = lds_off(smem + LDS::TRASH_OFF) + (uint32_t)(wave * 256 + lane * 4);
+    float* uslot = (float*)(smem + LDS::UNION_OFF) + wave * 512;  // this wave's two union slots
     int upq[2] = {-1, -1};  // deferred union bounds in flight (compact_regs / union_finish)
     // list counts and thresholds of this lane's two queries (compact_regs)
     ListRegs lr;
@@ -170,18 +172,6 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
             dma_norm_piece(decltype(NXT)::value ? nv_nxt : nv_cur, nslot_w + (uint32_t)(tnext & 3) * S_NSLOT_B);
     };
 
-    // a corpus piece fused with the MFMA pair before it (AsmMmaV::mma2_dma:
-    // the pair is the M0-write -> LDS-DMA wait state instead of an s_nop)
-    constexpr bool FUSE = LN == 1 && DT != F32 && !(ABL & (2 | 4 | 128));
-    auto mma_piece = [&](auto INITC, auto W, auto JP, auto NXT, uint32_t slot, f32x4& c0, f32x4& c1,
-                         const frag_t& a, const bfrag_t& b0, const bfrag_t& b1, const f32x4& ci) {
-        constexpr int init = decltype(INITC)::value, w = decltype(W)::value, jp = decltype(JP)::value;
-        static_assert(w < 4, "corpus pieces only");
-        const char* cb = decltype(NXT)::value ? cb_nxt : cb_cur;
-        const uint32_t m0 = m0w + slot * S_STAGE + w * 1024;
-        AsmMmaV<DT>::template mma2_dma<init, jp * STAGE_B>(c0, c1, a, b0, b1, ci, voffA, cb + w * 8 * RB, m0);
-    };
-
     // prologue: stages 0 .. NS-2 (all in tile 0: SPT >= NS - 1)
     static_for<NS - 1>([&](auto ST) {
         constexpr int st = decltype(ST)::value;
@@ -206,7 +196,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
     for (int n = 0; n < N; ++n) qloc[n] = qw0 + n * 16 + (lane & 15);
     const bool qv0 = q0 + qloc[0] < nq, qv1 = q0 + qloc[1] < nq;
     // per-lane LDS addresses: my two queries' list rows, my thresholds in a norm slot
-    const uint32_t lq[N] = {lst_off + (uint32_t)(qloc[0] * LCAP * 8), lst_off + (uint32_t)(qloc[1] * LCAP * 8)};
+    const uint32_t lq[N] = {ld_off + (uint32_t)(qloc[0] * LCAP * 4), ld_off + (uint32_t)(qloc[1] * LCAP * 4)};
+    const uint32_t li_d = li_off - ld_off;
     const uint32_t gt_lane = (uint32_t)(128 + (lane & 15) * 4);
     const uint32_t nrm_lane = (uint32_t)(rl0 * 4);
 
@@ -287,11 +278,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
             static_for<M>([&](auto MM) {
                 constexpr int m = decltype(MM)::value;
                 constexpr int INIT = j == 0 ? (METRIC == L2 ? 1 : 2) : 0;
-                constexpr bool FP = FUSE && (m == 4 || m == 6);  // pair m carries corpus piece m / 2 - 2
-                if constexpr (FP)
-                    mma_piece(std::integral_constant<int, INIT>{}, std::integral_constant<int, m / 2 - 2>{}, JP{},
-                              NXT{}, c4, acc[m][0], acc[m][1], X[m], b[kq0][0], b[kq0][1], yin[m]);
-                else if constexpr (!(ABL & 4))
+                if constexpr (!(ABL & 4))
                     AsmMmaV<DT>::template mma2<INIT>(acc[m][0], acc[m][1], X[m], b[kq0][0], b[kq0][1], yin[m]);
                 // half 1 of this stage: two reads per pair over the first four
                 // pairs, so the mid-stage wait finds them landed
@@ -312,7 +299,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                         static_for<4>([&](auto W) { piece(W, JP{}, NXT{}, c4, tnext); });
                         if constexpr (jp == 0) piece(std::integral_constant<int, 4>{}, JP{}, NXT{}, c4, tnext);
                     }
-                } else if constexpr (!FP) {  // a stage's corpus pieces after MFMA pairs 4, 6 (half 0) and 4, 5 (half 1)
+                } else {  // a stage's corpus pieces after MFMA pairs 4, 6 (half 0) and 4, 5 (half 1)
                     if constexpr (m == 4) piece(std::integral_constant<int, 0>{}, JP{}, NXT{}, c4, tnext);
                     if constexpr (m == 6) piece(std::integral_constant<int, 1>{}, JP{}, NXT{}, c4, tnext);
                 }
@@ -347,11 +334,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
             const uint32_t rd_next = lds_base + S_RING_OFF + c1 * S_STAGE + rd_lane;
             static_for<M>([&](auto MM) {
                 constexpr int m = decltype(MM)::value;
-                constexpr bool FP = FUSE && (m == 4 || m == 5);  // pair m carries corpus piece m - 2
-                if constexpr (FP)
-                    mma_piece(std::integral_constant<int, 0>{}, std::integral_constant<int, m - 2>{}, JP{}, NXT{}, c4,
-                              acc[m][0], acc[m][1], Y[m], b[kq0 + 1][0], b[kq0 + 1][1], yin[m]);
-                else if constexpr (!(ABL & 4))
+                if constexpr (!(ABL & 4))
                     AsmMmaV<DT>::template mma2<0>(acc[m][0], acc[m][1], Y[m], b[kq0 + 1][0], b[kq0 + 1][1], yin[m]);
                 // half 0 of stage g+1: two reads per pair over the first four
                 // pairs (X[2m+1]'s last reader is >= 8 MFMAs back)
@@ -360,8 +343,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                     ds_rd128<(2 * m + 1) * 2048>(X[2 * m + 1], rd_next);
                 }
                 if constexpr (!(ABL & 128)) {
-                    if constexpr (m == 4 && !FP) piece(std::integral_constant<int, 2>{}, JP{}, NXT{}, c4, tnext);
-                    if constexpr (m == 5 && !FP) piece(std::integral_constant<int, 3>{}, JP{}, NXT{}, c4, tnext);
+                    if constexpr (m == 4) piece(std::integral_constant<int, 2>{}, JP{}, NXT{}, c4, tnext);
+                    if constexpr (m == 5) piece(std::integral_constant<int, 3>{}, JP{}, NXT{}, c4, tnext);
                     if constexpr (m == 6 && jp == 0) piece(std::integral_constant<int, 4>{}, JP{}, NXT{}, c4, tnext);
                 }
             });
@@ -387,7 +370,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
         // acc[0..5] take 24 VALU instructions, so the last pairs' XDL writes
         // (acc[6], acc[7]) are >= 24 wait states old when read -- past the 11
         // (8-pass) / 19 (16-pass) states of the XDL-write -> VALU-read hazard,
-        // with no s_nop pad (acc_fence_v: ~80 cycles per tile)
+        // with no s_nop pad (acc_fence_v: ~80 cycles per tile; -1.6 % on (d))
 #pragma unroll
         for (int m = 0; m < M; ++m)
 #pragma unroll
@@ -405,8 +388,9 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                         keys[(q0 + qloc[n]) * ld + (int64_t)(ct0 + t) * TILE_R + rl0 + 16 * m + i] = acc[m][n][i];
         }
         // the tile's threshold reads (last stage, half 0) and the next
-        // stage's fragments have landed
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        // stage's fragments have landed (gr: operands, so that no use of the
+        // thresholds is scheduled above the wait)
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(gr[0]), "+v"(gr[1])::"memory");
         float tn[N];
         tn[0] = qv0 ? fminf(lr.tau[0], ord2f(gr[0])) : -FX_INF;
         tn[1] = qv1 ? fminf(lr.tau[1], ord2f(gr[1])) : -FX_INF;
@@ -420,7 +404,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
         if constexpr (ABL & 64) stq[12] += __builtin_amdgcn_s_memtime() - s_end;  // fast epilogue
         // union bounds of the last tile's compactions (their windows have landed)
         if (__builtin_expect(upq[0] >= 0 || upq[1] >= 0, 0))
-            union_finish(upq, ulds, lr, gtq, p.splits, split, p.prune_rank, p.union_w, lane);
+            union_finish(upq, uslot, lr, gtq, p.splits, split, p.prune_rank, p.union_w, lane);
         // unlikely: the slow path's code (pushes, compaction) is laid out
         // after the loop, so the hot path runs through without a jump over it
         // (the loop body then fits the instruction cache)
@@ -442,8 +426,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                     static_for<M>([&](auto MM) {
                         constexpr int m = decltype(MM)::value;
                         if (__builtin_amdgcn_ballot_w64(gmin[n][m] <= tn[n])) {
-                            ovf |= push_col<M, N>(acc, n, m, 15u, tn[n], trow0 + rl0 + m * 16, rlim, lq[n], lr.cnt[n],
-                                                  lane, pend[n]);
+                            ovf |= push_reg<M, N>(acc, n, m, 15u, tn[n], trow0 + rl0 + m * 16, rlim, lq[n], li_d, trash,
+                                                  lr.cnt[n], lane, pend[n]);
                             if constexpr (ABL & (64 | 1024)) stq[10] += 1;
                         }
                     });
@@ -456,8 +440,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
             while (__builtin_amdgcn_ballot_w64(need)) {
                 uint64_t s_cp = 0;
                 if constexpr (ABL & (64 | 1024)) s_cp = __builtin_amdgcn_s_memtime();
-                lr = compact_regs(lst, lr, p.share ? gtq : nullptr, qw0, lane, p.pub ? pubw : nullptr, p.splits,
-                                  split, p.prune_rank, cat, p.union_w, upq, ulds, p.union_defer);
+                lr = compact_regs(lst_d, lst_i, lr, p.share ? gtq : nullptr, qw0, lane, p.pub ? pubw : nullptr, p.splits,
+                                  split, p.prune_rank, cat, p.union_w, upq, uslot, p.union_defer);
                 if constexpr (ABL & (64 | 1024)) {
                     stq[8] += 1;
                     stq[9] += __builtin_amdgcn_s_memtime() - s_cp;
@@ -472,8 +456,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                         constexpr int m = decltype(MM)::value;
                         const unsigned el = (pn >> (4 * m)) & 15u;
                         if (__builtin_amdgcn_ballot_w64(el != 0u))
-                            ovf |= push_col<M, N>(acc, n, m, el, tq, trow0 + rl0 + m * 16, rlim, lq[n], lr.cnt[n],
-                                                  lane, pend[n]);
+                            ovf |= push_reg<M, N>(acc, n, m, el, tq, trow0 + rl0 + m * 16, rlim, lq[n], li_d, trash,
+                                                  lr.cnt[n], lane, pend[n]);
                     });
                 });
                 need = ovf;
@@ -508,9 +492,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
         if (q0 + q >= nq) break;
         const int cq = qi < 16 ? __builtin_amdgcn_readlane(lr.cnt[0], qi) : __builtin_amdgcn_readlane(lr.cnt[1], qi - 16);
         const int cn = min(cq, LCAP);
-        const uint2 e = lane < cn ? lst[q * LCAP + lane] : make_uint2(__float_as_uint(FX_INF), (unsigned)INT_MAX);
-        float d = __uint_as_float(e.x);
-        int i = (int)e.y;
+        float d = lane < cn ? lst_d[q * LCAP + lane] : FX_INF;
+        int i = lane < cn ? lst_i[q * LCAP + lane] : INT_MAX;
         sort64(d, i, lane);
         if (lane < KP) {
             p.cand_d[(obase + q) * KP + lane] = d;

@@ -107,19 +107,21 @@ __device__ __forceinline__ unsigned union_kth_v(const unsigned (&kv)[4], unsigne
     return hi;
 }
 
-// LDS store of one list entry (key, row) as one 8-byte word
-// (ds_write2_b32: the two words from any two registers, no aligned pair)
-__device__ __forceinline__ void ds_wr_entry(uint32_t off, float key, int row) {
-    asm volatile("ds_write2_b32 %0, %1, %2 offset1:1" ::"v"(off), "v"(key), "v"(row) : "memory");
+// LDS store through an explicit byte offset (the lean push below picks the
+// offset per lane instead of branching)
+__device__ __forceinline__ void ds_wr32(uint32_t off, float v) {
+    asm volatile("ds_write_b32 %0, %1" ::"v"(off), "v"(v) : "memory");
+}
+__device__ __forceinline__ void ds_wr32(uint32_t off, int v) {
+    asm volatile("ds_write_b32 %0, %1" ::"v"(off), "v"(v) : "memory");
 }
 
 // Per-wave candidate lists of k_scan_v4.  The wave owns 32 queries: query
 // column c of accumulator half n (lanes with lane & 15 == c, n = 0, 1) is
-// tile-local query qw0 + 16 n + c.  Each list lives in LDS ([query][LCAP]
-// entries of (key, row), 8 B each); its entry count and its pruning
-// threshold live in registers (cnt[n], tau[n]), the same value in the 4 lanes
-// that hold the query (lane >> 4 = 0..3: rows 4 (lane >> 4) + 16 m + i of the
-// tile), so a push reserves its slots without an LDS atomic round trip.
+// tile-local query qw0 + 16 n + c.  Each list lives in LDS ([query][LCAP] keys
+// and rows); its entry count and its pruning threshold live in registers
+// (cntv[n], tauv[n]), the same value in the 4 lanes that hold the query, so a
+// push reserves its slots without an LDS atomic round trip.
 
 // Exclusive prefix and total of `c` over the 4 lanes that hold one query
 // (lane >> 4 = 0..3, the same lane & 15).
@@ -131,45 +133,37 @@ __device__ __forceinline__ void quad_prefix(int c, int lane, int& excl, int& tot
     total = s2 + b;
 }
 
-// Push the keys of accumulator group (m, n) selected by `elig` (bit i: row
-// row0 + i) that pass `tn` into the lane's query list.  Records are rare
-// after a split's first tiles (a streaming top-k sees ~k ln(N/k) of them per
-// query), so the push walks the group's 4 rows one at a time and skips, on
-// one uniform branch, every row no lane passes on: a sparse group costs a
-// compare and a branch per row plus ~20 instructions per row that holds a
-// record.  Slots: the lanes of one query column that pass on the same row
-// are counted by the 4-lane prefix (permlane swaps); only the passing lanes
-// store (exec-masked).  Entries that find
-// the list full are recorded in `pend` (bit 4m + i) for a retry after the
-// compaction; the return value says whether any lane has one.
+// Push the entries of accumulator group (m, n) selected by `elig` (4 bits)
+// that pass `tn` into the lane's query list; entries that find the list full
+// are recorded in `pend` (bit 4m+i) for a retry after compaction (returns
+// whether any were).  Branch-free: every lane stores all 4 of its entries,
+// those that do not pass (or find the list full) into the wave's trash word.
+// lq: LDS byte offset of the query's key row; li_d: rows array - keys array.
 template <int M, int N>
-__device__ __forceinline__ bool push_col(const f32x4 (&acc)[M][N], int n, int m, unsigned elig, float tn, int row0,
-                                         int rlim, uint32_t lq, int& cntv, int lane, unsigned& pend) {
-    bool late = false;
+__device__ __forceinline__ bool push_reg(const f32x4 (&acc)[M][N], int n, int m, unsigned elig, float tn, int row0,
+                                         int rlim, uint32_t lq, uint32_t li_d, uint32_t trash, int& cntv, int lane,
+                                         unsigned& pend) {
+    unsigned msk = 0u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) msk |= (acc[m][n][i] <= tn && row0 + i < rlim) ? (1u << i) : 0u;
+    msk &= elig;
+    int excl, total;
+    quad_prefix((int)__popc(msk), lane, excl, total);
+    const int s = cntv + excl;
+    unsigned late = 0u;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const float key = acc[m][n][i];
-        const bool take = ((elig >> i) & 1u) && key <= tn && row0 + i < rlim;
-        const uint64_t T = __builtin_amdgcn_ballot_w64(take);
-        if (T == 0) continue;
-        // my column's lanes c, c + 16, c + 32, c + 48 among the takers
-        const uint32_t tl = (uint32_t)T >> (lane & 15), th = (uint32_t)(T >> 32) >> (lane & 15);
-        const int b0 = tl & 1, b1 = (tl >> 16) & 1, b2 = th & 1, b3 = (th >> 16) & 1;
-        const int r4 = lane >> 4;
-        const int excl = (r4 > 0 ? b0 : 0) + (r4 > 1 ? b1 : 0) + (r4 > 2 ? b2 : 0);
-        const int tot = b0 + b1 + b2 + b3;
-        const int slot = cntv + excl;
-        if (take) {
-            if (slot < LCAP) {
-                ds_wr_entry(lq + (uint32_t)slot * 8u, key, row0 + i);
-            } else {
-                pend |= 1u << (4 * m + i);
-                late = true;
-            }
-        }
-        cntv += tot;
+        const int slot = s + (int)__popc(msk & ((1u << i) - 1u));
+        const bool take = (msk >> i) & 1u;
+        const bool ok = take && slot < LCAP;
+        const uint32_t e = lq + (uint32_t)slot * 4u;
+        ds_wr32(ok ? e : trash, acc[m][n][i]);
+        ds_wr32(ok ? e + li_d : trash, row0 + i);
+        late |= (take && !ok) ? (1u << i) : 0u;
     }
-    return late;
+    cntv += total;
+    pend |= late << (4 * m);
+    return late != 0u;
 }
 
 // Compact this wave's lists that hold `at` or more entries (KP < at <= LCAP)
@@ -189,28 +183,24 @@ __device__ __forceinline__ bool push_col(const f32x4 (&acc)[M][N], int n, int m,
 // counting entries never over-counts rows).  A split that starts late then
 // prunes with what all earlier splits found.  rank (>= k): every dropped row
 // lies above the final shared threshold, which k_refine folds into its
-// certification bound (RefineParams.gtau).
+// certification bound (RefineParams.gtau).  The union reads of the full
+// lists are issued together (one memory round trip per 4 lists, not one per
+// list).
 //
-// The union bound does not wait for its reads: the window of up to two
-// compacted lists is fetched by LDS-DMA into the wave's two union slots
-// (ulds, 1 KiB each: the window's 256 keys, 4 per lane) and bounded at the
-// next tile's epilogue (union_finish) -- by then the DMA ring's counted
-// stage waits have retired it (>= 12 younger pieces, SPT >= 4 stages) -- so
-// the global round trip runs under the next tile's MFMAs instead of in the
-// slow path.  Lists past the two slots take the synchronous path below (one
-// memory round trip per 4 lists).  upq[u]: wave-local query of slot u, -1 free.
+// defer (option union_defer): the window of up to two compacted lists is
+// fetched by LDS-DMA into the wave's two union slots (1 KiB each: the
+// window's 256 keys, 4 per lane) and bounded at the next tile's epilogue
+// (union_finish) -- by then the DMA ring's counted stage waits have retired
+// it (>= 12 younger pieces, SPT >= 4 stages) -- so the global round trip runs
+// under the next tile's MFMAs instead of in the slow path.  upq[u]: the
+// wave-local query of slot u, -1 free.
 struct ListRegs {
     int cnt[2];
     float tau[2];
 };
 // log2 of the published keys each split of a union window contributes
 __device__ __forceinline__ int union_le(int uw) { return uw >= 64 ? 2 : uw >= 32 ? 3 : 4; }
-// one union window -> LDS: lane l moves 4 keys of list l >> (le - 2) (clamped to
-// list 0 past the window's last split; masked in union_finish)
-__device__ __forceinline__ void union_dma(const float* src, uint32_t lds) {
-    asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off sc1" ::"v"(src), "{m0}"(lds) : "memory");
-}
-__device__ __forceinline__ void union_finish(int (&upq)[2], uint32_t ulds, const ListRegs& r, unsigned* gtq,
+__device__ __forceinline__ void union_finish(int (&upq)[2], const float* uslot, const ListRegs& r, unsigned* gtq,
                                              int splits, int split, int rank, int uw, int lane) {
     const int le = union_le(uw);
     const int w0 = split & ~(uw - 1);
@@ -220,9 +210,9 @@ __device__ __forceinline__ void union_finish(int (&upq)[2], uint32_t ulds, const
     for (int u = 0; u < 2; ++u) {
         if (upq[u] < 0) continue;
         const int qi = upq[u];
-        f32x4 raw;
-        ds_rd128<0>(raw, ulds + (uint32_t)(u * 1024 + lane * 16));
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        // a compiler-visible LDS load: its consumers wait for it (an asm
+        // ds_read's result could be read before an asm lgkmcnt wait)
+        const f32x4 raw = *(const f32x4*)(uslot + u * 256 + lane * 4);
         unsigned kv[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) kv[j] = in_win ? f2ord(raw[j]) : 0xFFFFFFFFu;
@@ -232,9 +222,9 @@ __device__ __forceinline__ void union_finish(int (&upq)[2], uint32_t ulds, const
         upq[u] = -1;
     }
 }
-__device__ __forceinline__ ListRegs compact_regs(uint2* lst, ListRegs r, unsigned* gtq, int qw0, int lane,
+__device__ __forceinline__ ListRegs compact_regs(float* lst_d, int* lst_i, ListRegs r, unsigned* gtq, int qw0, int lane,
                                               float* pub, int splits, int split, int rank, int at, int uw,
-                                              int (&upq)[2], uint32_t ulds, int defer) {
+                                              int (&upq)[2], float* uslot, int defer) {
     int (&cntv)[2] = r.cnt;
     float (&tauv)[2] = r.tau;
     const uint64_t f0 = __builtin_amdgcn_ballot_w64(lane < 16 && cntv[0] >= at);
@@ -252,11 +242,13 @@ __device__ __forceinline__ ListRegs compact_regs(uint2* lst, ListRegs r, unsigne
         // LCAP lanes hold entries of this list (lanes past it would read the
         // next query's row)
         const bool live = lane < cq && lane < LCAP;
-        const uint2 e = live ? lst[q * LCAP + lane] : make_uint2(__float_as_uint(FX_INF), (unsigned)INT_MAX);
-        float d = __uint_as_float(e.x);
-        int i = (int)e.y;
+        float d = live ? lst_d[q * LCAP + lane] : FX_INF;
+        int i = live ? lst_i[q * LCAP + lane] : INT_MAX;
         sort64(d, i, lane);
-        if (lane < KP) lst[q * LCAP + lane] = make_uint2(__float_as_uint(d), (unsigned)i);
+        if (lane < KP) {
+            lst_d[q * LCAP + lane] = d;
+            lst_i[q * LCAP + lane] = i;
+        }
         const float dr = readlane_f(d, rank - 1);
         if ((lane & 15) == (qi & 15)) {
             if (qi < 16) { tauv[0] = dr; cntv[0] = KP; }
@@ -276,14 +268,17 @@ __device__ __forceinline__ ListRegs compact_regs(uint2* lst, ListRegs r, unsigne
     const int w0 = split & ~(uw - 1);
     const int nsp = splits - w0 < uw ? splits - w0 : uw;
     uint64_t rest = all;
-    // deferred: up to two windows fetched into the union slots (union_finish)
+    // deferred: up to two windows fetched into the union slots (union_finish),
+    // in the corpus pieces' form (scalar window base, per-lane byte offsets)
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
         if (rest == 0 || upq[u] >= 0 || !defer) continue;
         const int qi = __builtin_ctzll(rest);
         rest &= rest - 1;
         const int l = lane >> (le - 2), e4 = lane & ((1 << (le - 2)) - 1);
-        union_dma(pub + ((int64_t)qi * splits + w0 + (l < nsp ? l : 0)) * KP + 4 * e4, ulds + (uint32_t)(u * 1024));
+        const char* wb = sgpr_ptr((const char*)(pub + ((int64_t)qi * splits + w0) * KP));
+        const uint32_t voff = (uint32_t)(((l < nsp ? l : 0) * KP + 4 * e4) * 4);
+        dma_piece<0, 4>(voff, wb, lds_off(uslot + u * 256));  // s_nop 4: wb was written by VALU
         upq[u] = qi;
     }
     // the rest now, up to 4 lists per memory round trip
@@ -332,8 +327,7 @@ __device__ __forceinline__ ListRegs compact_regs(uint2* lst, ListRegs r, unsigne
 // among the asm MFMAs (the caller keeps >= 2 MFMA pairs between the last XDL
 // write of `a` and this read; hipcc does not see the asm MFMAs' hazards)
 // One asm block: the compiler pads an s_nop between two inline-asm blocks
-// where the second reads what the first wrote (it cannot see inside them);
-// inside one block the VALU -> VALU read needs no wait state.
+// where the second reads what the first wrote (it cannot see inside them).
 __device__ __forceinline__ float min4(const f32x4& a) {
     float r;
     asm volatile("v_min3_f32 %0, %1, %2, %3\n\tv_min_f32 %0, %0, %4"

@@ -44,13 +44,20 @@ def _candidate_lists_intact(request, monkeypatch):
         return
     from rag_faiss_embedding_amd import faiss
     orig = faiss._FlatIndex.search
-    dropped = []
+    dropped, pending = [], {}
 
-    def search(self, *a, **kw):
-        out = orig(self, *a, **kw)
-        dropped.append(self.last_dropped_candidates())
+    def search(self, x, *a, **kw):
+        out = orig(self, x, *a, **kw)
+        if faiss._is_device_tensor(x):
+            # stream-ordered: reading the count would synchronise inside the
+            # test (test_device_search_is_stream_ordered); read after it, for
+            # the index's last search
+            pending[id(self)] = self
+        else:
+            dropped.append(self.last_dropped_candidates())
         return out
 
     monkeypatch.setattr(faiss._FlatIndex, "search", search)
     yield
+    dropped.extend(ix.last_dropped_candidates() for ix in pending.values())
     assert not any(dropped), f"searches dropped corrupted candidate ids: {dropped}"

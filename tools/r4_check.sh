@@ -1,14 +1,18 @@
 #!/bin/bash
-# Round-4 GPU check: same-box A/B of the round-3 product (libfx_index_r3.so),
-# the round-4 push + deferred union bound (libfx_index_r4b.so, with and
-# without the deferral) and the current build (corpus pieces fused into MFMA
-# pairs), then the whole -m gpu suite on the current build.  Stops at the
-# first failure.
+# Round-4 GPU check: same-box A/B on (d), the N = 8 per-rank shard and (b) of
+# the round-3 product against the current build with the union bound waited
+# for in place (default) and deferred (union_defer = 1); the fallback counts
+# of every line; then the -m gpu suite on the current build.
 # usage: tools/r4_check.sh <tag>
 set -euo pipefail
 t=$1; o=gpurun_out/$t; mkdir -p $o
 L=rag-faiss-embedding_amd
-tools/r4_ab.sh ${t}ab "$L/libfx_index_r3.so|-" "$L/libfx_index_r4b.so|-" "$L/libfx_index_r4f.so|-" "$L/libfx_index.so|-"
+A=("$L/libfx_index_r3.so|-" "$L/libfx_index.so|-" "$L/libfx_index.so|FX_UNION_DEFER=1")
+BENCH_ARGS="--rows 1250000" tools/gpu_multi.sh ${t}ab_shard d "${A[@]}"
+python tools/show_fallbacks.py gpurun_out/${t}ab_shard
+tools/gpu_multi.sh ${t}ab_d d "${A[@]}"
+python tools/show_fallbacks.py gpurun_out/${t}ab_d
+tools/gpu_multi.sh ${t}ab_b b "${A[@]}"
 timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $o/pytest.log 2>&1
 tail -3 $o/pytest.log
 echo check done

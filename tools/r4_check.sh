@@ -10,6 +10,9 @@ L=rag-faiss-embedding_amd
 A=("$L/libfx_index_r3.so|-" "$L/libfx_index.so|-" "$L/libfx_index.so|FX_UNION_DEFER=1")
 BENCH_ARGS="--rows 1250000" tools/gpu_multi.sh ${t}ab_shard d "${A[@]}"
 python tools/show_fallbacks.py gpurun_out/${t}ab_shard
+# the deferred arm only where the shard certified every query (a broken bound
+# sends every query to the exact scan: minutes on (d))
+if grep -q "arm2_1.json fallbacks 0 " <(python tools/show_fallbacks.py gpurun_out/${t}ab_shard); then :; else A=("${A[@]:0:2}"); fi
 tools/gpu_multi.sh ${t}ab_d d "${A[@]}"
 python tools/show_fallbacks.py gpurun_out/${t}ab_d
 tools/gpu_multi.sh ${t}ab_b b "${A[@]}"

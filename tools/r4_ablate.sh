@@ -9,6 +9,6 @@ set -euo pipefail
 t=$1
 P=rag-faiss-embedding_amd/libfx_index.so
 A=rag-faiss-embedding_amd/libfx_index_abl.so
-tools/gpu_multi.sh ${t}_d d "$P|-" "$A|FX_SCAN_DBG=8" "$A|FX_SCAN_DBG=256" "$A|FX_SCAN_DBG=2" "$A|FX_SCAN_DBG=10"
+tools/gpu_multi.sh ${t}_d d "$P|-" "$A|FX_SCAN_DBG=8" "$A|FX_SCAN_DBG=256" "$A|FX_SCAN_DBG=2"
 BENCH_ARGS="--rows 1250000" tools/gpu_multi.sh ${t}_shard d "$P|-" "$A|FX_SCAN_DBG=8" "$A|FX_SCAN_DBG=256"
 echo ablate done

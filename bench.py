@@ -483,7 +483,8 @@ def main():
         except Exception as e:  # noqa: BLE001 -- a side measurement never breaks the bench line
             log("pcie-inclusive leg failed:", e)
         try:
-            out["latency_nq1"] = latency_nq1(ix, xq, I, k, args.latency_calls)
+            if args.latency_calls > 0:  # 0: skip (profiling runs keep only the bench's own launches)
+                out["latency_nq1"] = latency_nq1(ix, xq, I, k, args.latency_calls)
         except Exception as e:  # noqa: BLE001
             log("latency_nq1 leg failed:", e)
     if rank == 0 and not args.no_cpu:

@@ -11,7 +11,7 @@ tag=$1; shift
 out=gpurun_out/prof_$tag
 mkdir -p "$out"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-B="python3 bench.py --no-cpu $*"
+B="python3 bench.py --no-cpu --latency-calls 0 $*"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o run -- \
     $B > "$out/trace.log" 2>&1
 pmc() {  # <subdir> <counters...>

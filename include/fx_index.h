@@ -95,8 +95,8 @@ int fx_index_set_stream(FxIndex* index, void* stream);
  * hipGraph), "scan_place" -1/0/1, "scan_sx" >= 0, "reduce_cand" 0/1,
  * "f32_split" 0/1, "centre" 0/1, "scan_pub" 0/1, "prune_rank" 0..32,
  * "compact_at" 0 or 33..64 (list fill that triggers a compaction), "union_w"
- * 0/16/32/64 (splits per union-bound window), "union_defer" 0/1 (a
- * compaction's union bound fetched by LDS-DMA and bounded a tile later
+ * 0/16/32/64 (splits per union-bound window), "union_defer" 0/1 (default 1:
+ * a compaction's union bound fetched by LDS-DMA and bounded a tile later
  * instead of waited for).  None changes results, only
  * speed.  Unknown name or out-of-range value: FX_E_ARG.  (The diagnostic
  * build libfx_index_diag.so adds test hooks -- "force_fallback",

@@ -95,7 +95,7 @@ struct Options {
     int prune_rank = 0;      // FX_PRUNE_RANK: rank of the shared threshold (0: max(6k/5, 12))
     int compact_at = 0;      // FX_COMPACT_AT: list fill that triggers a compaction (0: default, KP < v <= CAP)
     int union_w = 0;         // FX_UNION_W: splits per union-bound window (16, 32, 64; 0: by split count)
-    int union_defer = 0;     // FX_UNION_DEFER: union bounds fetched by LDS-DMA, bounded a tile later
+    int union_defer = 1;     // FX_UNION_DEFER: union bounds fetched by LDS-DMA, bounded a tile later (0: in place)
     int graph_verbose = 0;   // FX_SEARCH_GRAPH_VERBOSE
 #ifdef FX_DIAG
     int force_fallback = 0;  // FX_FORCE_FALLBACK: flag every query (1: -> re-scan, 2: -> exact scan)

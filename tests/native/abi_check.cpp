@@ -178,8 +178,12 @@ int main() {
     OK(fx_index_set_option(ix, "compact_at", 40));
     OK(fx_index_set_option(ix, "union_w", 64));
     search_and_check(ix, xb, n, d, 64, 10, rng, "compact_at 40, union window 64");
+    OK(fx_index_set_option(ix, "union_defer", 0));
+    search_and_check(ix, xb, n, d, 64, 10, rng, "union bound in place");
+    CHECK(fx_index_set_option(ix, "union_defer", 2) == FX_E_ARG, "union_defer 2 accepted");
     OK(fx_index_set_option(ix, "compact_at", 0));
     OK(fx_index_set_option(ix, "union_w", 0));
+    OK(fx_index_set_option(ix, "union_defer", 1));
 
     // ---- IxF2 round trip, fp32 and bf16 storage ---------------------------
     const std::string path = std::string(getenv("TMPDIR") ? getenv("TMPDIR") : "/tmp") + "/fx_abi_check.bin";

@@ -10,7 +10,7 @@ for r in 1 2; do
   i=0
   for arm in "$@"; do
     lib=${arm%%|*}; envs=${arm#*|}; [ "$envs" = "-" ] && envs=""
-    env FX_INDEX_LIB=$lib $envs timeout -k 10 150 python -u bench.py --config $cfg ${BENCH_ARGS:-} --no-cpu --steps 6 --warmup 1 > $o/arm${i}_$r.json 2> $o/arm${i}_$r.err
+    env FX_INDEX_LIB=$lib $envs timeout -k 10 150 python -u bench.py --config $cfg ${BENCH_ARGS:-} --no-cpu --latency-calls 0 --steps 6 --warmup 1 > $o/arm${i}_$r.json 2> $o/arm${i}_$r.err
     echo "$i: $arm" >> $o/arms_$r.txt
     i=$((i+1))
   done

@@ -93,7 +93,7 @@ struct Options {
     int centre = 1;          // FX_CENTER: L2 scan images are centred on a row sample's mean
     int pub = 1;             // FX_SCAN_PUB: union threshold over published per-split lists
     int prune_rank = 0;      // FX_PRUNE_RANK: rank of the shared threshold (0: max(6k/5, 12))
-    int compact_at = 0;      // FX_COMPACT_AT: list fill that triggers a compaction (0: default, KP < v <= CAP)
+    int compact_at = 0;      // FX_COMPACT_AT: list fill that triggers a compaction (0: default 48, KP < v <= CAP)
     int union_w = 0;         // FX_UNION_W: splits per union-bound window (16, 32, 64; 0: by split count)
     int union_defer = 1;     // FX_UNION_DEFER: union bounds fetched by LDS-DMA, bounded a tile later (0: in place)
     int graph_verbose = 0;   // FX_SEARCH_GRAPH_VERBOSE
@@ -319,7 +319,10 @@ void plan_scan(const FxIndex* h, int64_t nq, int k, ScanParams& p) {
     p.sx = 0;
     p.pub = nullptr;
     p.prune_rank = KP;
-    p.compact_at = h->opt.compact_at > KP && h->opt.compact_at <= CAP ? h->opt.compact_at : CAP;
+    // default 48: with the union bound deferred a compaction is cheap enough
+    // that tightening the threshold 16 entries earlier pays (same-box sweep,
+    // profiles/r4/ab/compact_r4c.txt: (d) -1.1 %, (b) and the N = 8 shard -0.2 %)
+    p.compact_at = h->opt.compact_at > KP && h->opt.compact_at <= CAP ? h->opt.compact_at : 48;
     p.share = k <= KP ? 1 : 0;
     p.union_w = 16;
     p.union_defer = h->opt.union_defer;

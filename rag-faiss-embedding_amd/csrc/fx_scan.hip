@@ -366,17 +366,19 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
         });
 
         // ---- epilogue of tile t: the accumulator holds the keys ------------
-        // Group minima first, group by group (asm volatile: in this order):
-        // acc[0..5] take 24 VALU instructions, so the last pairs' XDL writes
-        // (acc[6], acc[7]) are >= 24 wait states old when read -- past the 11
-        // (8-pass) / 19 (16-pass) states of the XDL-write -> VALU-read hazard,
-        // with no s_nop pad (acc_fence_v: ~80 cycles per tile; -1.6 % on (d))
+        // The accumulator's XDL-write -> VALU-read wait states are padded in
+        // full (acc_fence_v) before the group minima read it.  Round 4 tried
+        // without the pad (the minima of acc[0..5] first, so the last pairs'
+        // results are >= 24 instructions old when read): (d) 0.7 % faster,
+        // but the fp16 instance of config (e) 11-14 % slower on three boxes
+        // (profiles/r4/ab/fence_r4fe.txt) -- more record tiles, as if some
+        // reads saw an accumulator before its last product; the pad stays.
+        acc_fence_v(acc);
 #pragma unroll
         for (int m = 0; m < M; ++m)
 #pragma unroll
             for (int n = 0; n < N; ++n) gmin[n][m] = min4(acc[m][n]);
         if (__builtin_expect(p.dbgbuf != nullptr, 0)) {  // diagnostics (FX_SCAN_DBG & 32): every key -> [nq_pad][cap rows]
-            acc_fence_v(acc);
             float* keys = (float*)p.dbgbuf;
             const int64_t ld = (int64_t)p.n_ctiles * TILE_R;
 #pragma unroll

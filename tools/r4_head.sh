@@ -22,4 +22,5 @@ for nq in 1 16 64 256; do
   timeout -k 10 200 python -u bench.py --nq $nq --steps 50 --warmup 5 --no-cpu --latency-calls 0 > $o/bench_d_nq$nq.json 2> $o/bench_d_nq$nq.err
 done
 timeout -k 10 600 tools/profile_scan.sh ${t}_d --steps 5 --warmup 2
+FX_PROFILE_MIN=1 timeout -k 10 600 tools/profile_scan.sh ${t}_e --config e --steps 3 --warmup 1
 echo head done

@@ -68,7 +68,8 @@ struct ScanLds {
 // valid, timing distorted by the stamps); 128 the stage's LDS-DMA pieces
 // issued as one burst after the first MFMA pair (results valid); 256 the
 // epilogue's fast path only (slow tiles counted into p.stamps, no pushes:
-// results invalid)
+// results invalid); 2048 no accumulator wait-state pad before the epilogue
+// (the round-4 variant; with 1024 for its slow-path stamps)
 //
 // LN selects the shape of the corpus LDS-DMA pieces and of the LDS image:
 //   LN = 0: fragment-shaped pieces (16 rows x 64 B: each piece touches 16
@@ -372,8 +373,9 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
         // results are >= 24 instructions old when read): (d) 0.7 % faster,
         // but the fp16 instance of config (e) 11-14 % slower on three boxes
         // (profiles/r4/ab/fence_r4fe.txt) -- more record tiles, as if some
-        // reads saw an accumulator before its last product; the pad stays.
-        acc_fence_v(acc);
+        // reads saw an accumulator before its last product; the pad stays
+        // (ABL & 2048: without it, for the stamps A/B of the ablation build).
+        if constexpr (!(ABL & 2048)) acc_fence_v(acc);
 #pragma unroll
         for (int m = 0; m < M; ++m)
 #pragma unroll
@@ -516,8 +518,10 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
 template <int DT, int METRIC, int KSTEPS, int ABL = 0, int LN = 1>
 static hipError_t scan_v4_t(const ScanParams& p, hipStream_t s) {
 #ifdef FX_ABLATION
-    if constexpr (ABL == 0 && DT == BF16 && METRIC == L2 && KSTEPS == 24) {
-        switch (p.dbg & 2047) {
+    if constexpr (ABL == 0 && METRIC == L2 && ((DT == BF16 && KSTEPS == 24) || (DT == F16 && KSTEPS == 12))) {
+        switch (p.dbg & 4095) {
+            case 2048: return scan_v4_t<DT, METRIC, KSTEPS, 2048, LN>(p, s);
+            case 3072: return scan_v4_t<DT, METRIC, KSTEPS, 3072, LN>(p, s);
             case 1: return scan_v4_t<DT, METRIC, KSTEPS, 1, LN>(p, s);
             case 9: return scan_v4_t<DT, METRIC, KSTEPS, 9, LN>(p, s);
             case 2: return scan_v4_t<DT, METRIC, KSTEPS, 2, LN>(p, s);

@@ -372,9 +372,9 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
         // without the pad (the minima of acc[0..5] first, so the last pairs'
         // results are >= 24 instructions old when read): (d) 0.7 % faster,
         // but the fp16 instance of config (e) 11-14 % slower on three boxes
-        // (profiles/r4/ab/fence_r4fe.txt) -- more record tiles, as if some
-        // reads saw an accumulator before its last product; the pad stays
-        // (ABL & 2048: without it, for the stamps A/B of the ablation build).
+        // (profiles/r4/ab/fence_r4fe.txt).  Stamps (ABL & 2048, pad_stamps_
+        // r4s.txt): the same record tiles and fewer cycles per tile, but
+        // lower clocks -- the pad's idle cycles keep the clock up; it stays.
         if constexpr (!(ABL & 2048)) acc_fence_v(acc);
 #pragma unroll
         for (int m = 0; m < M; ++m)

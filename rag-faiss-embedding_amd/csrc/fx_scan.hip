@@ -69,7 +69,8 @@ struct ScanLds {
 // issued as one burst after the first MFMA pair (results valid); 256 the
 // epilogue's fast path only (slow tiles counted into p.stamps, no pushes:
 // results invalid); 2048 no accumulator wait-state pad before the epilogue
-// (the round-4 variant; with 1024 for its slow-path stamps)
+// (the round-4 variant; with 1024 for its slow-path stamps); 8192 the pad
+// twice (results valid: the power/clock A/B)
 //
 // LN selects the shape of the corpus LDS-DMA pieces and of the LDS image:
 //   LN = 0: fragment-shaped pieces (16 rows x 64 B: each piece touches 16
@@ -376,6 +377,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
         // r4s.txt): the same record tiles and fewer cycles per tile, but
         // lower clocks -- the pad's idle cycles keep the clock up; it stays.
         if constexpr (!(ABL & 2048)) acc_fence_v(acc);
+        if constexpr (ABL & 8192) acc_fence_v(acc);  // ablation: a second pad (power A/B)
 #pragma unroll
         for (int m = 0; m < M; ++m)
 #pragma unroll
@@ -519,9 +521,10 @@ template <int DT, int METRIC, int KSTEPS, int ABL = 0, int LN = 1>
 static hipError_t scan_v4_t(const ScanParams& p, hipStream_t s) {
 #ifdef FX_ABLATION
     if constexpr (ABL == 0 && METRIC == L2 && ((DT == BF16 && KSTEPS == 24) || (DT == F16 && KSTEPS == 12))) {
-        switch (p.dbg & 4095) {
+        switch (p.dbg & 16383) {
             case 2048: return scan_v4_t<DT, METRIC, KSTEPS, 2048, LN>(p, s);
             case 3072: return scan_v4_t<DT, METRIC, KSTEPS, 3072, LN>(p, s);
+            case 8192: return scan_v4_t<DT, METRIC, KSTEPS, 8192, LN>(p, s);
             case 1: return scan_v4_t<DT, METRIC, KSTEPS, 1, LN>(p, s);
             case 9: return scan_v4_t<DT, METRIC, KSTEPS, 9, LN>(p, s);
             case 2: return scan_v4_t<DT, METRIC, KSTEPS, 2, LN>(p, s);

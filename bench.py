@@ -55,7 +55,7 @@ CONFIGS = {
 # exact-oracle recall sample per config (>= 1000 queries where the
 # oracle allows; the full-corpus streaming oracle costs ~0.25 s per query on (d)
 # and ~1.3 s on (e) with 16 host cores: the (e) leg takes ~5 min)
-RECALL_QUERIES = {"d": 256, "b": 1000, "e": 256}
+RECALL_QUERIES = {"d": 1000, "b": 1000, "e": 256}
 SHORT_DT = {"float32": "f32", "bfloat16": "bf16", "float16": "f16"}
 # MI355X_MICROARCH.md: dense MFMA peaks (TFLOP/s) and HBM3E peak (GB/s)
 MFMA_PEAK = {"float32": 157.3, "bfloat16": 2500.0, "float16": 2500.0}
@@ -290,22 +290,56 @@ def latency_nq1(ix, xq, I_dev, k, calls):
             "ids_match_device_path": same == calls}
 
 
+def latency_nq1_f32(calls, device, n=100_000, d=384, k=10, nq=1000):
+    """latency_nq1 on the reference's own storage dtype and call shape: an fp32
+    IndexFlatL2(384) (faiss_store.py:29, rag_datastore_manager.py:138) of
+    config-(c) size, one numpy float32 query per call (faiss_store.py:61-64,
+    rag_datastore_manager.py:215-218), host D / I out; every call's ids
+    checked against the device-resident batch search of the same queries."""
+    ix = fx.IndexFlatL2(d, device=device.index)
+    buf = torch.empty((n, d), dtype=torch.float32, device=device)
+    fx.synth_fill(buf, 0, CORPUS_SEED)
+    ix.add(buf)
+    del buf
+    xq = torch.empty((nq, d), dtype=torch.float32, device=device)
+    fx.synth_fill(xq, 0, QUERY_SEED)
+    _, I = ix.search(xq, k)
+    r = latency_nq1(ix, xq, I, k, calls)
+    r["index"] = f"{n} x {d} fp32 IndexFlatL2 (the reference's storage dtype), synthetic rows"
+    del ix
+    return r
+
+
 def read_pmc_traffic(cfg_name, n_local, nq, data="synthetic"):
     """HBM bytes per scan launch from a committed rocprofv3 --pmc summary of
-    this same workload (profiles/pmc_scan_<cfg>[_clustered].json), or None."""
+    this same workload (profiles/pmc_scan_<cfg>[_clustered].json), and where
+    that figure comes from: (bytes, source) or (None, None).  The figure is a
+    lookup of an earlier profiled run, not a counter of this one; `source`
+    names its file, the scan's rocprof mean duration and the effective clock
+    of that profiled run (GRBM_GUI_ACTIVE / 8 / wall)."""
     base = f"pmc_scan_{cfg_name}{'' if data == 'synthetic' else '_' + data}"
     p = ROOT / "profiles" / f"{base}_nq{nq}.json"  # a small-batch sweep point
     if not p.exists():
         p = ROOT / "profiles" / f"{base}.json"
     if not p.exists():
-        return None
+        return None, None
     try:
         j = json.loads(p.read_text())
-        if j.get("rows_per_gpu") == n_local and j.get("nq") == nq:
-            return j.get("hbm_bytes_per_launch")
+        if j.get("rows_per_gpu") != n_local or j.get("nq") != nq:
+            return None, None
+        src = {"file": str(p.relative_to(ROOT)), "summary": j.get("source"),
+               "note": "committed rocprofv3 --pmc pass of the same workload (not this run)"}
+        summ = ROOT / j["source"] if j.get("source") else None
+        if summ is not None and summ.exists():
+            sj = json.loads(summ.read_text())
+            scan = sj.get("kernels", {}).get(sj.get("scan_kernel"), {})
+            src["kernel_ms"] = round(scan["avg_ms"], 3) if "avg_ms" in scan else None
+            clk = sj.get("effective_clock_ghz")
+            src["clock_ghz"] = round(clk, 3) if clk else None
+            src["l2_hit_rate"] = round(sj["l2_hit_rate"], 3) if sj.get("l2_hit_rate") else None
+        return j.get("hbm_bytes_per_launch"), src
     except Exception:  # noqa: BLE001
-        return None
-    return None
+        return None, None
 
 
 def main():
@@ -428,7 +462,8 @@ def main():
                 "frac": round(gbs / HBM_PEAK_GBS, 4)}
     # the committed PMC pass measured the default scan: no traffic figure for an opt-in variant
     variant = os.environ.get("FX_F32_SPLIT", "1") == "0"
-    roof["traffic"] = None if variant else read_pmc_traffic(args.config, n_local, nq, args.data)
+    roof["traffic"], roof["traffic_source"] = (None, None) if variant else \
+        read_pmc_traffic(args.config, n_local, nq, args.data)
     roof["kernel"] = "k_scan_v4" + \
         (" F32S (fp32 as 3 bf16 MFMA products)" if split else "") + \
         " (fused MFMA distance GEMM + top-k select)"
@@ -487,6 +522,11 @@ def main():
                 out["latency_nq1"] = latency_nq1(ix, xq, I, k, args.latency_calls)
         except Exception as e:  # noqa: BLE001
             log("latency_nq1 leg failed:", e)
+        try:
+            if args.latency_calls > 0:
+                out["latency_nq1_f32"] = latency_nq1_f32(args.latency_calls, device)
+        except Exception as e:  # noqa: BLE001
+            log("latency_nq1_f32 leg failed:", e)
     if rank == 0 and not args.no_cpu:
         nthreads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
         extra = cpu_baseline_and_recall(args, n_total, d, dtype, k, D, I, xq, nthreads, device)

@@ -57,7 +57,9 @@ enum {
     FX_E_HIP = -2,      /* HIP runtime failure / no device                            */
     FX_E_IO = -3,       /* file open / read / write / format error                     */
     FX_E_UNSUPPORTED = -4,
-    FX_E_OOM = -5
+    FX_E_OOM = -5,
+    FX_E_INTEGRITY = -6 /* a host-output search whose candidate lists held row ids outside
+                           [0, ntotal): its top-k may be missing rows (never in a correct build) */
 };
 
 /* Largest k served by the fused scan path (per query).  fx_index_search
@@ -126,7 +128,9 @@ int fx_index_add(FxIndex* index, int64_t n, const void* x, int x_dtype, int x_me
  * is stream-ordered: it enqueues its work and returns without waiting for
  * the device (the exact fallback for uncertified queries is decided on the
  * device).  Workspace growth (first search of a larger shape) may
- * synchronise through hipMalloc / hipFree. */
+ * synchronise through hipMalloc / hipFree; so does a k > FX_MAX_K search
+ * whose sort workspace exceeds 512 MiB (it is released after the call, a
+ * smaller one is kept for the next). */
 int fx_index_search(FxIndex* index, int64_t nq, const void* q, int q_dtype, int q_mem,
                     int k, float* D, int64_t* I, int out_mem);
 
@@ -141,8 +145,10 @@ int fx_index_last_exact_fallbacks(FxIndex* index, int64_t* out);
  * dropped because their row id (other than the empty-slot -1) lay outside
  * [0, ntotal).  Always 0 unless a scan list was corrupted; the dropped
  * entries are never gathered, so a non-zero count means the top-k may be
- * missing rows and must be treated as an error by the caller (faiss itself
- * cannot return such a result: faiss_store.py:64). */
+ * missing rows (faiss itself cannot return such a result: faiss_store.py:64).
+ * A host-output search (FX_MEM_HOST) checks it itself and returns
+ * FX_E_INTEGRITY; after a device-resident search the caller must read it
+ * (this call synchronises the index stream). */
 int fx_index_last_dropped_candidates(FxIndex* index, int64_t* out);
 
 /* IndexFlatL2 reset (faiss_store.py:124-128). Keeps the HBM allocation. */

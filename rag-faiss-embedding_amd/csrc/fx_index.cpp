@@ -714,6 +714,14 @@ hipError_t dump_device(const std::string& path, const void* dev, size_t n) {
 }
 #endif
 
+// a host-output search whose refine dropped candidate ids outside [0, ntotal)
+// (a corrupted scan list): the top-k may be missing rows, so it is an error
+// (include/fx_index.h, fx_index_last_dropped_candidates)
+int integrity_error(const FxIndex* h) {
+    return set_err(FX_E_INTEGRITY, "search: %lld candidate row ids outside [0, %lld) were dropped (corrupted scan list)",
+                   (long long)h->last_dropped, (long long)h->ntotal);
+}
+
 int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int k, float* D, int64_t* I,
               int out_mem) {
     hipStream_t s = h->stream();
@@ -801,12 +809,14 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
         h->last_exact = h->pin_nf[1];
         h->last_dropped = h->pin_nf[2];
         h->fb_pending = false;
+        if (h->last_dropped > 0) return integrity_error(h);
     }
     return FX_OK;
 }
 
 // k > FX_BIG_K: exact keys of every (query, row) pair and a radix sort per
 // query (fx_hugek.hip).  Every result is exact, so no query is "uncertified".
+constexpr size_t HK_KEEP_BYTES = (size_t)512 << 20;
 int do_search_hugek(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int k, float* D, int64_t* I,
                     int out_mem) {
     hipStream_t s = h->stream();
@@ -844,10 +854,13 @@ int do_search_hugek(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_me
     p.D = Dd;
     p.I = Id;
     HIP_TRY(launch_hugek_search(p, h->hk_ws.p, h->hk_ws.bytes, qb, s));
-    // the sort keys (up to 2 GiB + rocPRIM temporaries) are not kept past the
-    // call: k > FX_MAX_K is the rare caller's path (hipFree waits for the stream)
-    HIP_TRY(hipStreamSynchronize(s));
-    h->hk_ws.release();
+    // the sort keys + rocPRIM temporaries stay cached for the next call up to
+    // HK_KEEP_BYTES; a larger workspace (up to 2 GiB of keys) is released
+    // after the call, which waits for the stream (hipFree would anyway)
+    if (h->hk_ws.bytes > HK_KEEP_BYTES) {
+        HIP_TRY(hipStreamSynchronize(s));
+        h->hk_ws.release();
+    }
     h->last_fallbacks = 0;
     h->last_exact = 0;
     h->last_dropped = 0;
@@ -961,7 +974,7 @@ int graph_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int k, floa
         h->last_exact = h->ghnf[1];
         h->last_dropped = h->ghnf[2];
         h->fb_pending = false;
-        return FX_OK;
+        return h->last_dropped > 0 ? integrity_error(h) : FX_OK;
     }
     const int rc = do_search(h, nq, q, q_dtype, FX_MEM_HOST, k, D, I, FX_MEM_HOST);
     if (rc == FX_OK && !h->gfailed) {
@@ -1216,6 +1229,7 @@ static int read_counts(FxIndex* h) {
         h->last_exact = h->pin_nf[1];
         h->last_dropped = h->pin_nf[2];
         h->fb_pending = false;
+        if (h->last_dropped > 0) return integrity_error(h);
     }
     return FX_OK;
 }

@@ -54,10 +54,10 @@ template <int NS>
 struct ScanLds {
     // LDS-DMA destinations first (norm slots, ring, union slots), then the lists
     static constexpr int UNION_OFF = S_RING_OFF + NS * S_STAGE;  // [4 waves][2 slots][256 keys] (compact_regs)
-    static constexpr int LD_OFF = UNION_OFF + 4 * 2 * 1024;
-    static constexpr int LI_OFF = LD_OFF + TILE_Q * LCAP * 4;
-    static constexpr int TRASH_OFF = LI_OFF + TILE_Q * LCAP * 4;  // [4 waves][64 lanes] sink of the branch-free push
-    static constexpr int BYTES = TRASH_OFF + 4 * 256;
+    static constexpr int LST_OFF = UNION_OFF + 4 * 2 * 1024;  // [TILE_Q][LCAP keys | LCAP rows]
+    // [4 waves][keys 64 lanes | rows 64 lanes]: sink of the branch-free push
+    static constexpr int TRASH_OFF = LST_OFF + TILE_Q * LSTRIDE * 4;
+    static constexpr int BYTES = TRASH_OFF + 4 * 2 * 256;
     static_assert(BYTES <= 160 * 1024, "LDS budget");
 };
 
@@ -70,7 +70,7 @@ struct ScanLds {
 // epilogue's fast path only (slow tiles counted into p.stamps, no pushes:
 // results invalid); 2048 no accumulator wait-state pad before the epilogue
 // (the round-4 variant; with 1024 for its slow-path stamps); 8192 the pad
-// twice (results valid: the power/clock A/B)
+// twice (results valid: the power/clock A/B; with 1024: 9216)
 //
 // LN selects the shape of the corpus LDS-DMA pieces and of the LDS image:
 //   LN = 0: fragment-shaped pieces (16 rows x 64 B: each piece touches 16
@@ -110,11 +110,10 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
     const int64_t q0 = (int64_t)qtile * TILE_Q;
     if (p.trace && tid == 0) trace_block_start(p, qtile, split);
 
-    float* lst_d = (float*)(smem + LDS::LD_OFF);
-    int* lst_i = (int*)(smem + LDS::LI_OFF);
+    float* lst = (float*)(smem + LDS::LST_OFF);
     const int qw0 = wave * 32;  // this wave's queries (tile-local)
-    const uint32_t ld_off = lds_off(lst_d), li_off = lds_off(lst_i);
-    const uint32_t trash = lds_off(smem + LDS::TRASH_OFF) + (uint32_t)(wave * 256 + lane * 4);
+    const uint32_t ld_off = lds_off(lst);
+    const uint32_t trash = lds_off(smem + LDS::TRASH_OFF) + (uint32_t)(wave * 512 + lane * 4);
     float* uslot = (float*)(smem + LDS::UNION_OFF) + wave * 512;  // this wave's two union slots
     int upq[2] = {-1, -1};  // deferred union bounds in flight (compact_regs / union_finish)
     // list counts and thresholds of this lane's two queries (compact_regs)
@@ -198,8 +197,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
     for (int n = 0; n < N; ++n) qloc[n] = qw0 + n * 16 + (lane & 15);
     const bool qv0 = q0 + qloc[0] < nq, qv1 = q0 + qloc[1] < nq;
     // per-lane LDS addresses: my two queries' list rows, my thresholds in a norm slot
-    const uint32_t lq[N] = {ld_off + (uint32_t)(qloc[0] * LCAP * 4), ld_off + (uint32_t)(qloc[1] * LCAP * 4)};
-    const uint32_t li_d = li_off - ld_off;
+    const uint32_t lq[N] = {ld_off + (uint32_t)(qloc[0] * LSTRIDE * 4), ld_off + (uint32_t)(qloc[1] * LSTRIDE * 4)};
     const uint32_t gt_lane = (uint32_t)(128 + (lane & 15) * 4);
     const uint32_t nrm_lane = (uint32_t)(rl0 * 4);
 
@@ -233,8 +231,14 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
     // compaction calls, compaction cycles, group pushes, -}
     // [11]: slow path up to the first compaction; [12]: fast epilogue (tile end -> ballot decided)
     uint64_t stq[15] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    // ABL & 1024: stamps in the slow path only ([6]-[11]) + [13] wave cycles, [14] tiles
-    if constexpr (ABL & 1024) stq[13] = __builtin_amdgcn_s_memtime();
+    // ABL & 1024: stamps in the slow path only ([6]-[11]) + [13] wave cycles,
+    // [14] tiles, [12] the wave's wall time in s_memrealtime ticks (100 MHz):
+    // the in-kernel clock is [13] / [12] x 100 MHz (MI355X_MICROARCH.md,
+    // "DVFS give-back" item 6)
+    if constexpr (ABL & 1024) {
+        stq[12] = __builtin_amdgcn_s_memrealtime();
+        stq[13] = __builtin_amdgcn_s_memtime();
+    }
     uint64_t s_end = 0;
     for (int t = 0; t < ntiles; ++t) {
         unsigned gr[N];
@@ -398,15 +402,11 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
         // thresholds is scheduled above the wait)
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(gr[0]), "+v"(gr[1])::"memory");
         float tn[N];
-        tn[0] = qv0 ? fminf(lr.tau[0], ord2f(gr[0])) : -FX_INF;
-        tn[1] = qv1 ? fminf(lr.tau[1], ord2f(gr[1])) : -FX_INF;
+        tn[0] = qv0 ? min_raw(lr.tau[0], ord2f(gr[0])) : -FX_INF;
+        tn[1] = qv1 ? min_raw(lr.tau[1], ord2f(gr[1])) : -FX_INF;
         float mn[N];
 #pragma unroll
-        for (int n = 0; n < N; ++n) {
-            mn[n] = gmin[n][0];
-#pragma unroll
-            for (int m = 1; m < M; ++m) mn[n] = __builtin_fminf(mn[n], gmin[n][m]);
-        }
+        for (int n = 0; n < N; ++n) mn[n] = min8_raw(gmin[n]);
         if constexpr (ABL & 64) stq[12] += __builtin_amdgcn_s_memtime() - s_end;  // fast epilogue
         // union bounds of the last tile's compactions (their windows have landed)
         if (__builtin_expect(upq[0] >= 0 || upq[1] >= 0, 0))
@@ -422,18 +422,32 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
             uint64_t s_sl = 0;
             if constexpr (ABL & (64 | 1024)) s_sl = __builtin_amdgcn_s_memtime();
             const int trow0 = (ct0 + t) * TILE_R;
-            const int rlim = p.ntotal < (int64_t)trow0 + TILE_R ? (int)p.ntotal : trow0 + TILE_R;
-            {
+            // the index's last tile: rows past ntotal (zero rows of the padding)
+            // get key +inf, so no push tests a row bound (L2 padding keys are
+            // +inf already through their +inf norms; IP keys are 0)
+            if (__builtin_expect((int64_t)trow0 + TILE_R > p.ntotal, 0)) {
+                const int lim = (int)(p.ntotal - trow0);
+#pragma unroll
+                for (int m = 0; m < M; ++m)
+#pragma unroll
+                    for (int n = 0; n < N; ++n)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i)
+                            if (rl0 + 16 * m + i >= lim) acc[m][n][i] = FX_INF;
+            }
+            int rb = trow0 + rl0;  // row of acc[0][*][0] in this lane
             unsigned pend[N] = {0u, 0u};
-            bool ovf = false;
+            unsigned ovf = 0u;
             static_for<N>([&](auto NN) {
                 constexpr int n = decltype(NN)::value;
                 if (__builtin_amdgcn_ballot_w64(mn[n] <= tn[n])) {
                     static_for<M>([&](auto MM) {
                         constexpr int m = decltype(MM)::value;
                         if (__builtin_amdgcn_ballot_w64(gmin[n][m] <= tn[n])) {
-                            ovf |= push_reg<M, N>(acc, n, m, 15u, tn[n], trow0 + rl0 + m * 16, rlim, lq[n], li_d, trash,
-                                                  lr.cnt[n], lane, pend[n]);
+                            const unsigned late =
+                                push_group<false>(acc[m][n], 15u, tn[n], rb + 16 * m, lq[n], trash, lr.cnt[n], lane);
+                            pend[n] |= late << (4 * m);
+                            ovf |= late;
                             if constexpr (ABL & (64 | 1024)) stq[10] += 1;
                         }
                     });
@@ -442,17 +456,20 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
             if constexpr (ABL & (64 | 1024)) stq[11] += __builtin_amdgcn_s_memtime() - s_sl;
             // compact every list that reached p.compact_at (and any that overflowed)
             const int cat = min(p.compact_at, LCAP);  // the plan's trigger, within this kernel's lists
-            bool need = ovf || lr.cnt[0] >= cat || lr.cnt[1] >= cat;
-            while (__builtin_amdgcn_ballot_w64(need)) {
+            bool need = ovf != 0u || lr.cnt[0] >= cat || lr.cnt[1] >= cat;
+            while (__builtin_expect(__builtin_amdgcn_ballot_w64(need) != 0, 0)) {
                 uint64_t s_cp = 0;
                 if constexpr (ABL & (64 | 1024)) s_cp = __builtin_amdgcn_s_memtime();
-                lr = compact_regs(lst_d, lst_i, lr, p.share ? gtq : nullptr, qw0, lane, p.pub ? pubw : nullptr, p.splits,
-                                  split, p.prune_rank, cat, p.union_w, upq, uslot, p.union_defer);
+                lr = compact_regs(lst, lr, p.share ? gtq : nullptr, qw0, lane, p.pub ? pubw : nullptr, p.splits, split,
+                                  p.prune_rank, cat, p.union_w, upq, uslot, p.union_defer);
                 if constexpr (ABL & (64 | 1024)) {
                     stq[8] += 1;
                     stq[9] += __builtin_amdgcn_s_memtime() - s_cp;
                 }
-                ovf = false;
+                // the row base opaque here: nothing of the retry is hoisted
+                // in front of the loop (precomputed row ids spilled SGPRs)
+                asm volatile("" : "+v"(rb));
+                ovf = 0u;
                 static_for<N>([&](auto NN) {
                     constexpr int n = decltype(NN)::value;
                     const float tq = (n == 0 ? qv0 : qv1) ? fminf(lr.tau[n], tn[n]) : -FX_INF;
@@ -461,13 +478,15 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                     static_for<M>([&](auto MM) {
                         constexpr int m = decltype(MM)::value;
                         const unsigned el = (pn >> (4 * m)) & 15u;
-                        if (__builtin_amdgcn_ballot_w64(el != 0u))
-                            ovf |= push_reg<M, N>(acc, n, m, el, tq, trow0 + rl0 + m * 16, rlim, lq[n], li_d, trash,
-                                                  lr.cnt[n], lane, pend[n]);
+                        if (__builtin_amdgcn_ballot_w64(el != 0u)) {
+                            const unsigned late =
+                                push_group<true>(acc[m][n], el, tq, rb + 16 * m, lq[n], trash, lr.cnt[n], lane);
+                            pend[n] |= late << (4 * m);
+                            ovf |= late;
+                        }
                     });
                 });
-                need = ovf;
-            }
+                need = ovf != 0u;
             }
             if constexpr (ABL & (64 | 1024)) {
                 stq[6] += 1;
@@ -489,7 +508,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
     }
 
     // retire the ring's look-ahead pieces: an LDS-DMA still in flight at exit
-    // would land in the LDS of the next workgroup on this CU
+    // would land in the LDS of the next workgroup on this CU (a deferred union
+    // window still pending in upq is dropped unbounded: see compact_regs)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // final flush: sorted top-KP per query of this (query tile, split)
     const int64_t obase = ((int64_t)qtile * p.splits + split) * TILE_Q;
@@ -498,8 +518,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
         if (q0 + q >= nq) break;
         const int cq = qi < 16 ? __builtin_amdgcn_readlane(lr.cnt[0], qi) : __builtin_amdgcn_readlane(lr.cnt[1], qi - 16);
         const int cn = min(cq, LCAP);
-        float d = lane < cn ? lst_d[q * LCAP + lane] : FX_INF;
-        int i = lane < cn ? lst_i[q * LCAP + lane] : INT_MAX;
+        float d = lane < cn ? lst[q * LSTRIDE + lane] : FX_INF;
+        int i = lane < cn ? ((const int*)lst)[q * LSTRIDE + LCAP + lane] : INT_MAX;
         sort64(d, i, lane);
         if (lane < KP) {
             p.cand_d[(obase + q) * KP + lane] = d;
@@ -509,6 +529,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
     if (p.trace && tid == 0) p.trace[blockIdx.x * 4 + 3] = wall_clock64();
     if constexpr (ABL & 1024) {
         stq[13] = __builtin_amdgcn_s_memtime() - stq[13];
+        stq[12] = __builtin_amdgcn_s_memrealtime() - stq[12];
         stq[14] = (uint64_t)ntiles;
     }
     if constexpr (ABL & (64 | 256 | 1024)) {
@@ -525,6 +546,7 @@ static hipError_t scan_v4_t(const ScanParams& p, hipStream_t s) {
             case 2048: return scan_v4_t<DT, METRIC, KSTEPS, 2048, LN>(p, s);
             case 3072: return scan_v4_t<DT, METRIC, KSTEPS, 3072, LN>(p, s);
             case 8192: return scan_v4_t<DT, METRIC, KSTEPS, 8192, LN>(p, s);
+            case 9216: return scan_v4_t<DT, METRIC, KSTEPS, 9216, LN>(p, s);
             case 1: return scan_v4_t<DT, METRIC, KSTEPS, 1, LN>(p, s);
             case 9: return scan_v4_t<DT, METRIC, KSTEPS, 9, LN>(p, s);
             case 2: return scan_v4_t<DT, METRIC, KSTEPS, 2, LN>(p, s);

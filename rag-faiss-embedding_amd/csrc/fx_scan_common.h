@@ -107,19 +107,10 @@ __device__ __forceinline__ unsigned union_kth_v(const unsigned (&kv)[4], unsigne
     return hi;
 }
 
-// LDS store through an explicit byte offset (the lean push below picks the
-// offset per lane instead of branching)
-__device__ __forceinline__ void ds_wr32(uint32_t off, float v) {
-    asm volatile("ds_write_b32 %0, %1" ::"v"(off), "v"(v) : "memory");
-}
-__device__ __forceinline__ void ds_wr32(uint32_t off, int v) {
-    asm volatile("ds_write_b32 %0, %1" ::"v"(off), "v"(v) : "memory");
-}
-
 // Per-wave candidate lists of k_scan_v4.  The wave owns 32 queries: query
 // column c of accumulator half n (lanes with lane & 15 == c, n = 0, 1) is
-// tile-local query qw0 + 16 n + c.  Each list lives in LDS ([query][LCAP] keys
-// and rows); its entry count and its pruning threshold live in registers
+// tile-local query qw0 + 16 n + c.  Each list lives in LDS ([query][LCAP keys |
+// LCAP rows]); its entry count and its pruning threshold live in registers
 // (cntv[n], tauv[n]), the same value in the 4 lanes that hold the query, so a
 // push reserves its slots without an LDS atomic round trip.
 
@@ -133,37 +124,52 @@ __device__ __forceinline__ void quad_prefix(int c, int lane, int& excl, int& tot
     total = s2 + b;
 }
 
-// Push the entries of accumulator group (m, n) selected by `elig` (4 bits)
-// that pass `tn` into the lane's query list; entries that find the list full
-// are recorded in `pend` (bit 4m+i) for a retry after compaction (returns
-// whether any were).  Branch-free: every lane stores all 4 of its entries,
-// those that do not pass (or find the list full) into the wave's trash word.
-// lq: LDS byte offset of the query's key row; li_d: rows array - keys array.
-template <int M, int N>
-__device__ __forceinline__ bool push_reg(const f32x4 (&acc)[M][N], int n, int m, unsigned elig, float tn, int row0,
-                                         int rlim, uint32_t lq, uint32_t li_d, uint32_t trash, int& cntv, int lane,
-                                         unsigned& pend) {
-    unsigned msk = 0u;
+// A query's list in LDS: LCAP keys, then LCAP row ids (LSTRIDE words), so one
+// ds_write2_b32 (offset1 = LCAP dwords) stores an entry's key and row.
+constexpr int LSTRIDE = 2 * LCAP;
+__device__ __forceinline__ void ds_wr_entry(uint32_t off, float key, int row) {
+    asm volatile("ds_write2_b32 %0, %1, %2 offset1:%3" ::"v"(off), "v"(key), "v"(row), "i"(LCAP) : "memory");
+}
+
+// Push the 4 entries of one accumulator group (this lane's rows row0 .. row0+3
+// of its query) that pass `tn` (and, RETRY, are selected by `elig`) into the
+// query's list.  Entries that find the list full are returned as bits in
+// `late` for a retry after compaction (the caller ORs them into pend at bit
+// 4m+i).  Branch-free per lane: a lane stores all 4 entries, those that do not
+// pass into the wave's trash slot (trash .. trash + 4 LCAP); the rare group
+// that could overflow a list takes the per-entry slot check.  Rows of the
+// index's padding never pass: the caller sets their keys to +inf (the edge
+// tile), so no row bound is tested here.
+template <bool RETRY>
+__device__ __forceinline__ unsigned push_group(const f32x4& a, unsigned elig, float tn, int row0, uint32_t lq,
+                                               uint32_t trash, int& cntv, int lane) {
+    bool p[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) msk |= (acc[m][n][i] <= tn && row0 + i < rlim) ? (1u << i) : 0u;
-    msk &= elig;
+    for (int i = 0; i < 4; ++i) p[i] = (!RETRY || ((elig >> i) & 1u)) && a[i] <= tn;
+    const int c = (int)p[0] + (int)p[1] + (int)p[2] + (int)p[3];
     int excl, total;
-    quad_prefix((int)__popc(msk), lane, excl, total);
+    quad_prefix(c, lane, excl, total);
     const int s = cntv + excl;
-    unsigned late = 0u;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int slot = s + (int)__popc(msk & ((1u << i) - 1u));
-        const bool take = (msk >> i) & 1u;
-        const bool ok = take && slot < LCAP;
-        const uint32_t e = lq + (uint32_t)slot * 4u;
-        ds_wr32(ok ? e : trash, acc[m][n][i]);
-        ds_wr32(ok ? e + li_d : trash, row0 + i);
-        late |= (take && !ok) ? (1u << i) : 0u;
-    }
     cntv += total;
-    pend |= late << (4 * m);
-    return late != 0u;
+    unsigned late = 0u;
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(s + c > LCAP) == 0, 1)) {
+        uint32_t e = lq + (uint32_t)s * 4u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            ds_wr_entry(p[i] ? e : trash, a[i], row0 + i);
+            e += p[i] ? 4u : 0u;
+        }
+    } else {
+        int slot = s;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const bool ok = p[i] && slot < LCAP;
+            ds_wr_entry(ok ? lq + (uint32_t)slot * 4u : trash, a[i], row0 + i);
+            late |= (p[i] && !ok) ? (1u << i) : 0u;
+            slot += (int)p[i];
+        }
+    }
+    return late;
 }
 
 // Compact this wave's lists that hold `at` or more entries (KP < at <= LCAP)
@@ -193,7 +199,15 @@ __device__ __forceinline__ bool push_reg(const f32x4 (&acc)[M][N], int n, int m,
 // (union_finish) -- by then the DMA ring's counted stage waits have retired
 // it (>= 12 younger pieces, SPT >= 4 stages) -- so the global round trip runs
 // under the next tile's MFMAs instead of in the slow path.  upq[u]: the
-// wave-local query of slot u, -1 free.
+// wave-local query of slot u, -1 free.  The window's LDS-DMA is a plain
+// (non-coherent) global_load_lds, unlike the in-place path's agent-scope
+// atomic loads, so it may see an older version of a published list from this
+// XCD's L2.  That is safe by monotonicity: pub is reset to +inf before every
+// search and a split only ever republishes a list whose entry i is <= the
+// previous one's entry i (the KP best of a superset), so a stale entry is a
+// larger key, i.e. a looser but still valid bound.  Windows still pending
+// when a block's tile loop ends are not bounded (the bound only prunes; a
+// skipped one costs speed, never a result).
 struct ListRegs {
     int cnt[2];
     float tau[2];
@@ -222,9 +236,11 @@ __device__ __forceinline__ void union_finish(int (&upq)[2], const float* uslot, 
         upq[u] = -1;
     }
 }
-__device__ __forceinline__ ListRegs compact_regs(float* lst_d, int* lst_i, ListRegs r, unsigned* gtq, int qw0, int lane,
+__device__ __forceinline__ ListRegs compact_regs(float* lst, ListRegs r, unsigned* gtq, int qw0, int lane,
                                               float* pub, int splits, int split, int rank, int at, int uw,
                                               int (&upq)[2], float* uslot, int defer) {
+    float* lst_d = lst;                // keys of query q at q * LSTRIDE
+    int* lst_i = (int*)(lst + LCAP);   // rows of query q at q * LSTRIDE
     int (&cntv)[2] = r.cnt;
     float (&tauv)[2] = r.tau;
     const uint64_t f0 = __builtin_amdgcn_ballot_w64(lane < 16 && cntv[0] >= at);
@@ -242,12 +258,12 @@ __device__ __forceinline__ ListRegs compact_regs(float* lst_d, int* lst_i, ListR
         // LCAP lanes hold entries of this list (lanes past it would read the
         // next query's row)
         const bool live = lane < cq && lane < LCAP;
-        float d = live ? lst_d[q * LCAP + lane] : FX_INF;
-        int i = live ? lst_i[q * LCAP + lane] : INT_MAX;
+        float d = live ? lst_d[q * LSTRIDE + lane] : FX_INF;
+        int i = live ? lst_i[q * LSTRIDE + lane] : INT_MAX;
         sort64(d, i, lane);
         if (lane < KP) {
-            lst_d[q * LCAP + lane] = d;
-            lst_i[q * LCAP + lane] = i;
+            lst_d[q * LSTRIDE + lane] = d;
+            lst_i[q * LSTRIDE + lane] = i;
         }
         const float dr = readlane_f(d, rank - 1);
         if ((lane & 15) == (qi & 15)) {
@@ -319,6 +335,22 @@ __device__ __forceinline__ ListRegs compact_regs(float* lst_d, int* lst_i, ListR
             if (lane == 0 && v < own) gmin_u32(gtq + qi, v);
         }
     }
+    return r;
+}
+
+// minima without fminf's operand canonicalisation (a v_max per operand: the
+// compiler cannot see that asm results are canonical)
+__device__ __forceinline__ float min_raw(float a, float b) {
+    float r;
+    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float min8_raw(const float (&g)[8]) {
+    float r;
+    asm("v_min3_f32 %0, %1, %2, %3\n\tv_min3_f32 %0, %0, %4, %5\n\t"
+        "v_min3_f32 %0, %0, %6, %7\n\tv_min_f32 %0, %0, %8"
+        : "=&v"(r)
+        : "v"(g[0]), "v"(g[1]), "v"(g[2]), "v"(g[3]), "v"(g[4]), "v"(g[5]), "v"(g[6]), "v"(g[7]));
     return r;
 }
 

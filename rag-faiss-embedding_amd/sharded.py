@@ -114,8 +114,23 @@ class ShardedIndexFlatL2:
         return Dm, Im
 
     def search(self, xq, k: int):
-        """Global top-k: local scan -> exchange (one all_gather + merge)."""
-        D, I = self.local.search(xq, k)
+        """Global top-k: local scan -> exchange (one all_gather + merge).
+
+        Host queries under RCCL (the reference's numpy call form,
+        faiss_store.py:61-64): the queries go to this rank's GPU once, the
+        local scan, the all_gather and the merge stay on the device, and the
+        merged lists come back in ONE device-to-host copy (numpy in -> numpy
+        out, a host tensor -> host tensors)."""
         if self.world == 1:
-            return D, I
+            return self.local.search(xq, k)
+        host_in = not (isinstance(xq, torch.Tensor) and xq.is_cuda)
+        if host_in and dist.get_backend(self.group) == "nccl":
+            is_np = not isinstance(xq, torch.Tensor)
+            xt = torch.from_numpy(np.ascontiguousarray(xq, dtype=np.float32)) if is_np else xq
+            dev = self.comm_device(xt)
+            D, I = self.local.search(xt.to(dev), k)
+            Dm, Im = self.exchange(D, I, k)
+            Dm, Im = Dm.cpu(), Im.cpu()
+            return (Dm.numpy(), Im.numpy()) if is_np else (Dm, Im)
+        D, I = self.local.search(xq, k)
         return self.exchange(D, I, k)

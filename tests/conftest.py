@@ -15,6 +15,8 @@ GOLDEN = ROOT / "tests" / "golden"
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP C-ABI)")
     config.addinivalue_line("markers", "slow: long-running")
+    config.addinivalue_line("markers", "stream_ordered: device searches must not synchronise inside the test "
+                                       "(their candidate-integrity count is read at teardown)")
 
 
 @pytest.fixture(scope="session")
@@ -46,14 +48,15 @@ def _candidate_lists_intact(request, monkeypatch):
     orig = faiss._FlatIndex.search
     dropped, pending = [], {}
 
+    defer = request.node.get_closest_marker("stream_ordered") is not None
+
     def search(self, x, *a, **kw):
         out = orig(self, x, *a, **kw)
-        if faiss._is_device_tensor(x):
-            # stream-ordered: reading the count would synchronise inside the
-            # test (test_device_search_is_stream_ordered); read after it, for
-            # the index's last search
+        if defer and faiss._is_device_tensor(x):
+            # a test of stream ordering: reading the count would synchronise
+            # inside it; read at teardown, for the index's last search
             pending[id(self)] = self
-        else:
+        else:  # every other search: its own count (a device search syncs here)
             dropped.append(self.last_dropped_candidates())
         return out
 

@@ -129,6 +129,7 @@ def test_forced_fallback_many_queries(diag_fx, monkeypatch):
     assert_parity(D, I, Dr, Ir)
 
 
+@pytest.mark.stream_ordered
 def test_device_search_is_stream_ordered(fx, torch_cuda):
     """FX_MEM_DEVICE search enqueues and returns: queued behind a ~0.1 s spin
     kernel on the same stream, the call comes back while that stream is still

@@ -36,9 +36,10 @@ def rows(kind, n, d, seed):
 
 
 @pytest.mark.parametrize("kind", ["uniform", "clustered"])
-@pytest.mark.parametrize("dtype", ["bfloat16", "float32"])
-def test_compaction_and_union_options_exact(fx, kind, dtype):
-    n, d, nq, k = 300_000, 256, 300, 10
+# float16 at d = 384: the fp16 12-K-step scan instance of config (e)
+@pytest.mark.parametrize("dtype,d", [("bfloat16", 256), ("float32", 256), ("float16", 384)])
+def test_compaction_and_union_options_exact(fx, kind, dtype, d):
+    n, nq, k = 300_000, 300, 10
     xb = rows(kind, n, d, 11)
     xq = rows(kind, nq, d, 12)
     ix = fx.IndexFlatL2(d, dtype=dtype)

@@ -140,3 +140,44 @@ def test_exchange_buffers_follow_the_backend(monkeypatch):
     assert calls == [torch.device("cpu")]
     assert isinstance(Dm, np.ndarray) and isinstance(Im, np.ndarray)
     assert Im.tolist() == [[7, 1007, 3]] and Dm.tolist() == [[0.5, 0.5, 1.0]]
+
+
+def test_host_queries_under_rccl_stay_on_the_device(monkeypatch):
+    """Host (numpy) queries under the nccl backend: the local search is handed
+    the queries as a tensor on the exchange's device (not numpy), the
+    all_gather and the merge run there, and the merged lists are converted to
+    numpy once at the end (no host round trip of the local lists).  The
+    comm device is the CPU here; the GPU suite's RCCL tests run it for real."""
+    from rag_faiss_embedding_amd.sharded import ShardedIndexFlatL2
+    monkeypatch.setattr(dist, "is_initialized", lambda: True)
+    monkeypatch.setattr(dist, "get_world_size", lambda g=None: 2)
+    monkeypatch.setattr(dist, "get_rank", lambda g=None: 0)
+    monkeypatch.setattr(dist, "get_backend", lambda g=None: "nccl")
+    monkeypatch.setattr(ShardedIndexFlatL2, "comm_device", lambda self, like: torch.device("cpu"))
+    seen = []
+
+    class _TensorShard(_OracleShard):
+        def search(self, xq, k):
+            seen.append(type(xq))
+            D, I = super().search(xq.numpy(), k)
+            return torch.from_numpy(D), torch.from_numpy(I)
+
+    def merge(Dg, Ig, k):
+        assert isinstance(Dg, torch.Tensor) and isinstance(Ig, torch.Tensor)
+        Dm, Im = F.merge_topk(list(Dg.numpy()), list(Ig.numpy()), k)
+        return torch.from_numpy(Dm), torch.from_numpy(Im)
+
+    rng = np.random.default_rng(3)
+    xb = rng.standard_normal((50, 8)).astype(np.float32)
+    ix = ShardedIndexFlatL2(8, 100, local_index=_TensorShard(8, 0), merge_fn=merge)
+    ix.add(xb)
+    calls = []
+    monkeypatch.setattr(dist, "all_gather_into_tensor", _fake_gather(calls, 2))
+    xq = rng.standard_normal((4, 8))  # float64: converted like faiss (float32)
+    D, I = ix.search(xq, 5)
+    assert seen == [torch.Tensor] and len(calls) == 1
+    assert isinstance(D, np.ndarray) and isinstance(I, np.ndarray)
+    Dr, Ir = F.knn_exact(xq.astype(np.float32), xb, 5)
+    # rank 1's lists are rank 0's with ids + 1000 (the fake gather): ties at
+    # equal distance keep the smaller id
+    assert (I[:, 0] == Ir[:, 0]).all() and (D[:, 0] == Dr[:, 0]).all()

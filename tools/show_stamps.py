@@ -34,3 +34,7 @@ if a.shape[1] > 14 and a[:, 13].sum() > 0:  # ABL & 1024: slow-path-only stamps 
           f"{100 * a[:, 7].sum() / tot.sum():.2f} % of wave cycles ({a[:, 7].sum() / max(a[:, 6].sum(), 1):.0f} per slow tile; "
           f"before compaction {a[:, 11].sum() / max(a[:, 6].sum(), 1):.0f})")
     print(f"  compactions {a[:, 8].sum() / a[:, 14].sum():.5f} per wave-tile, {a[:, 9].sum() / max(a[:, 8].sum(), 1):.0f} cyc each")
+    if a[:, 12].sum() > 0:  # s_memrealtime ticks (100 MHz) of each wave's life
+        clk = a[:, 13] / np.maximum(a[:, 12], 1) * 0.1
+        print(f"  in-kernel clock {np.median(clk):.3f} GHz median over waves (p10 {np.percentile(clk, 10):.3f}, "
+              f"p90 {np.percentile(clk, 90):.3f}; s_memtime / s_memrealtime x 100 MHz)")

@@ -458,7 +458,8 @@ struct SearchPlan {
     RefineParams rp2{};
     PrepParams pp2{};
     int* n_exact = nullptr;  // queries the re-scan left uncertified too (-> exact scan)
-    int64_t nq_rescan = 0;   // flagged queries the re-scan takes (the rest: exact scan)
+    int nchunks = 0;         // re-scan chunks of <= RESCAN_MAX flagged queries each
+    int* chunk_cnt = nullptr;  // [nchunks] live queries of each chunk (k_rescan_chunks, on the device)
 };
 
 // The re-scan of the queries pass 1 could not certify (rows flag_list[0 ..
@@ -468,10 +469,12 @@ struct SearchPlan {
 // certification bound sits near the k1-th key instead of the ~2k-th.  Its
 // uncertified queries go to the exact scan.  Launched always; every kernel
 // reads the flagged count and exits at once when it is 0.
-// The re-scan's workspace is sized for at most RESCAN_MAX flagged queries,
-// whatever the batch (its lists are k1/4 splits wide): flagged queries past
-// that go straight to the exact scan (k_rescan_overflow), so a large batch
-// never pays for a re-scan workspace it almost never uses.
+// The re-scan's workspace is sized for RESCAN_MAX flagged queries whatever
+// the batch (its lists are k1/4 splits wide); a batch that could flag more
+// runs it in ceil(nq / RESCAN_MAX) chunks over the flagged list, each chunk's
+// live count decided on the device (k_rescan_chunks: empty chunks exit at
+// once), so a large batch never pays for a workspace it almost never uses
+// and never sends re-scannable queries to the exact scan.
 hipError_t plan_rescan(FxIndex* h, SearchPlan& P) {
     hipError_t e;
     const int64_t nq = std::min<int64_t>(P.nq, RESCAN_MAX), nq_pad = round_up(nq, QPAD);
@@ -483,8 +486,9 @@ hipError_t plan_rescan(FxIndex* h, SearchPlan& P) {
     if ((e = h->rq_rho.ensure((size_t)nq * 4)) != hipSuccess) return e;
     if ((e = h->rq_shift.ensure((size_t)nq * 8)) != hipSuccess) return e;
     if ((e = h->rq_gtau.ensure((size_t)nq_pad * 4)) != hipSuccess) return e;
-    if ((e = h->rq_flag.ensure((size_t)(P.nq + 1) * 4)) != hipSuccess) return e;  // every query may go exact
-    P.nq_rescan = nq;
+    P.nchunks = (int)((P.nq + RESCAN_MAX - 1) / RESCAN_MAX);
+    // [count | every query may go exact | the chunks' live counts]
+    if ((e = h->rq_flag.ensure((size_t)(P.nq + 1 + P.nchunks) * 4)) != hipSuccess) return e;
     PrepParams& pp = P.pp2;
     pp = P.pp;
     pp.nq = nq;
@@ -532,6 +536,7 @@ hipError_t plan_rescan(FxIndex* h, SearchPlan& P) {
     rp.nq_dev = n_flag;
     rp.out_idx = P.rp.flag_list;
     P.n_exact = (int*)h->rq_flag.p;
+    P.chunk_cnt = P.n_exact + 1 + P.nq;
     rp.n_flag = P.n_exact;
     rp.flag_list = P.n_exact + 1;
     rp.force_fb = h->opt.force_fallback == 2;
@@ -686,15 +691,24 @@ hipError_t enqueue_search(FxIndex* h, SearchPlan& P, hipStream_t s, bool timed, 
 #ifdef FX_ABLATION
     if ((P.sp.dbg & ~32) != 0) return hipSuccess;  // ablated scans: results invalid, no fallback chain
 #endif
-    if ((e = launch_prep_queries(P.pp2, s)) != hipSuccess) return e;
-    if ((e = hipMemsetD32Async((hipDeviceptr_t)P.sp2.gtau, 0xff800000u, (size_t)P.pp2.nq_pad, s)) != hipSuccess)
-        return e;
-    if ((e = launch_scan(P.scan_dt, h->metric, P.sp2, s)) != hipSuccess) return e;
+    if ((e = launch_rescan_chunks(P.rp.n_flag, (int)RESCAN_MAX, P.nchunks, P.chunk_cnt, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(P.n_exact, 0, 4, s)) != hipSuccess) return e;
-    if (P.nq_rescan < P.nq &&
-        (e = launch_rescan_overflow(P.rp.n_flag, (int)P.nq_rescan, P.n_exact, s)) != hipSuccess)
-        return e;
-    if ((e = launch_refine(h->dtype, h->metric, P.rp2, s)) != hipSuccess) return e;
+    for (int c = 0; c < P.nchunks; ++c) {  // chunk c: flagged queries [c RESCAN_MAX, ...)
+        const int* list = P.rp.flag_list + (size_t)c * RESCAN_MAX;
+        PrepParams pp = P.pp2;
+        pp.qidx = list;
+        pp.nq_dev = P.chunk_cnt + c;
+        ScanParams sp = P.sp2;
+        sp.nq_dev = P.chunk_cnt + c;
+        RefineParams rp2 = P.rp2;
+        rp2.nq_dev = P.chunk_cnt + c;
+        rp2.out_idx = list;
+        if ((e = launch_prep_queries(pp, s)) != hipSuccess) return e;
+        if ((e = hipMemsetD32Async((hipDeviceptr_t)sp.gtau, 0xff800000u, (size_t)pp.nq_pad, s)) != hipSuccess)
+            return e;
+        if ((e = launch_scan(P.scan_dt, h->metric, sp, s)) != hipSuccess) return e;
+        if ((e = launch_refine(h->dtype, h->metric, rp2, s)) != hipSuccess) return e;
+    }
     return launch_exact_fallback(h->dtype, h->metric, h->codes, h->row_bytes, h->kdim, h->ntotal, P.rp.qf32,
                                  P.n_exact, P.k, h->id_offset, (float*)h->fbc_d.p, (int*)h->fbc_i.p, P.rp.D, P.rp.I,
                                  s);

@@ -124,12 +124,12 @@ __host__ __device__ inline int fb_splits_for(int nf, int64_t ntotal) {
     return s < 1 ? 1 : s;
 }
 
-// the re-scan of uncertified queries takes at most this many of them per
-// search (its workspace is sized for it); the rest go to the exact scan
+// the re-scan of uncertified queries takes them in chunks of at most this
+// many (its workspace is sized for one chunk)
 constexpr int64_t RESCAN_MAX = 2048;
-// flagged queries [cap, n_flag[0]) of a search -> the exact scan's list
-// (n_exact[0] count, list at n_exact + 1); device-gated like the fallbacks
-hipError_t launch_rescan_overflow(const int* n_flag, int cap, int* n_exact, hipStream_t s);
+// counts[c] = live queries of re-scan chunk c: the flagged queries
+// [c cap, min(n_flag[0], (c+1) cap)); device-gated like the fallbacks
+hipError_t launch_rescan_chunks(const int* n_flag, int cap, int nchunks, int* counts, hipStream_t s);
 
 // True on a thread that is capturing a search into a hipGraph (fx_index.cpp
 // graph_build): the scan launchers then skip hipFuncSetAttribute, which the

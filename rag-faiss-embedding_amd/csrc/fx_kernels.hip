@@ -828,17 +828,17 @@ __global__ __launch_bounds__(256) void k_reduce_cand(const float* __restrict__ c
 }
 
 // flagged queries past the re-scan's capacity go straight to the exact scan
-__global__ __launch_bounds__(256) void k_rescan_overflow(const int* __restrict__ n_flag, int cap,
-                                                         int* __restrict__ n_exact) {
+__global__ __launch_bounds__(256) void k_rescan_chunks(const int* __restrict__ n_flag, int cap, int nchunks,
+                                                       int* __restrict__ counts) {
     const int nf = n_flag[0];
-    for (int i = cap + (int)(blockIdx.x * blockDim.x + threadIdx.x); i < nf; i += (int)(gridDim.x * blockDim.x)) {
-        const int pos = atomicAdd(n_exact, 1);
-        n_exact[1 + pos] = n_flag[1 + i];
+    for (int c = (int)threadIdx.x; c < nchunks; c += (int)blockDim.x) {
+        const int left = nf - c * cap;
+        counts[c] = left <= 0 ? 0 : (left < cap ? left : cap);
     }
 }
 
-hipError_t launch_rescan_overflow(const int* n_flag, int cap, int* n_exact, hipStream_t s) {
-    hipLaunchKernelGGL(k_rescan_overflow, dim3(64), dim3(256), 0, s, n_flag, cap, n_exact);
+hipError_t launch_rescan_chunks(const int* n_flag, int cap, int nchunks, int* counts, hipStream_t s) {
+    hipLaunchKernelGGL(k_rescan_chunks, dim3(1), dim3(256), 0, s, n_flag, cap, nchunks, counts);
     return hipGetLastError();
 }
 

@@ -35,6 +35,19 @@
 
 #include <stdlib.h>
 
+// the epilogue's accumulator wait-state pad (acc_fence_v): 1 in the product;
+// 0 only in A/B builds (make OUT=... CXXFLAGS=-DFX_EPILOGUE_PAD=0)
+#ifndef FX_EPILOGUE_PAD
+#define FX_EPILOGUE_PAD 1
+#endif
+// Each tile's first stage barrier taken at the end of the previous tile,
+// BEFORE its slow path, covering the next tile's stages 0 and 1 (1 in the
+// product; 0 in A/B builds: one barrier at the start of every stage).  See
+// the tile-end block in k_scan_v4.
+#ifndef FX_EARLY_BARRIER
+#define FX_EARLY_BARRIER 1
+#endif
+
 namespace fx {
 
 // DMA ring slots (NS - 1 stages in flight).  Measured: a
@@ -196,13 +209,20 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
 #pragma unroll
     for (int n = 0; n < N; ++n) qloc[n] = qw0 + n * 16 + (lane & 15);
     const bool qv0 = q0 + qloc[0] < nq, qv1 = q0 + qloc[1] < nq;
+    const uint64_t qm0 = __builtin_amdgcn_ballot_w64(qv0), qm1 = __builtin_amdgcn_ballot_w64(qv1);
     // per-lane LDS addresses: my two queries' list rows, my thresholds in a norm slot
     const uint32_t lq[N] = {ld_off + (uint32_t)(qloc[0] * LSTRIDE * 4), ld_off + (uint32_t)(qloc[1] * LSTRIDE * 4)};
     const uint32_t gt_lane = (uint32_t)(128 + (lane & 15) * 4);
     const uint32_t nrm_lane = (uint32_t)(rl0 * 4);
 
-    // stage 0 (4 corpus pieces + the norm piece) landed: younger are stages 1 .. NS-2
-    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"(4 * (NS - 2)) : "memory");
+    // EB: stages 0, 1 and 2 (+ the norm piece) landed for every wave, younger
+    // are stage 3's 4 pieces -- the tile-end barrier's guarantee (below) for
+    // tile 0.  Otherwise stage 0 landed, younger are stages 1 .. NS-2.
+    constexpr bool EB = FX_EARLY_BARRIER != 0;
+    if constexpr (EB)
+        asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+    else
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"i"(4 * (NS - 2)) : "memory");
     __builtin_amdgcn_sched_barrier(0);
     // fragment-read lane offset within a stage slot (half 0); half 1 is at
     // + rd_h1 (LN = 0: the next 1 KiB block; LN = 1: chunk + 4 under the
@@ -216,6 +236,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
         static_for<M>([&](auto MM) {
             constexpr int m = decltype(MM)::value;
             ds_rd128<m * 2048>(X[m], rd_addr);
+            if constexpr (EB) ds_rd128<m * 2048>(Y[m], rd_addr + rd_h1);  // stage 0's half 1 too
         });
         // row norms of tile 0 (rows rl0 + 16 m .. +3): [wave w][row%32] layout
         const uint32_t na = lds_base + S_NORM_OFF + nrm_lane;
@@ -265,10 +286,16 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                 s_a = __builtin_amdgcn_s_memtime();
                 if (j == 0 && s_end) stq[4] += s_a - s_end;
             }
-            if constexpr (ABL & 16)
+            if constexpr (EB && j == 0) {
+                // stage 0: X and Y in registers, stages 1 and 2 landed for every
+                // wave (the tile-end barrier): nothing to wait for
+            } else if constexpr (EB && j == 1) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // X of stage 1 (read in stage 0)
+            } else if constexpr (ABL & 16) {
                 asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(W) : "memory");
-            else
+            } else {
                 asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(W) : "memory");
+            }
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (ABL & 64) {
                 s_b = __builtin_amdgcn_s_memtime();
@@ -288,7 +315,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                     AsmMmaV<DT>::template mma2<INIT>(acc[m][0], acc[m][1], X[m], b[kq0][0], b[kq0][1], yin[m]);
                 // half 1 of this stage: two reads per pair over the first four
                 // pairs, so the mid-stage wait finds them landed
-                if constexpr (m < M / 2) {
+                if constexpr (m < M / 2 && !(EB && j == 0)) {  // EB: stage 0's Y read at the tile end
                     const uint32_t rd1 = rd_addr + rd_h1;
                     ds_rd128<(2 * m) * 2048>(Y[2 * m], rd1);
                     ds_rd128<(2 * m + 1) * 2048>(Y[2 * m + 1], rd1);
@@ -380,7 +407,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
         // (profiles/r4/ab/fence_r4fe.txt).  Stamps (ABL & 2048, pad_stamps_
         // r4s.txt): the same record tiles and fewer cycles per tile, but
         // lower clocks -- the pad's idle cycles keep the clock up; it stays.
-        if constexpr (!(ABL & 2048)) acc_fence_v(acc);
+        if constexpr (FX_EPILOGUE_PAD && !(ABL & 2048)) acc_fence_v(acc);
         if constexpr (ABL & 8192) acc_fence_v(acc);  // ablation: a second pad (power A/B)
 #pragma unroll
         for (int m = 0; m < M; ++m)
@@ -400,10 +427,35 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
         // the tile's threshold reads (last stage, half 0) and the next
         // stage's fragments have landed (gr: operands, so that no use of the
         // thresholds is scheduled above the wait)
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(gr[0]), "+v"(gr[1])::"memory");
+        if constexpr (EB) {
+            // The next tile's first barrier, taken here, before this tile's
+            // slow path: a wave with record tiles then holds its partners only
+            // from the next tile's stage 2 on (two stages of slack, ~1.2k
+            // cycles), instead of at once.  It needs what the barriers of
+            // stages 0 and 1 would have given: every wave's pieces of stages
+            // 1 and 2 landed (younger: stage 3's 4 pieces, issued in this
+            // tile's last stage), and every wave done with the ring slots those
+            // stages' DMA overwrites (this tile's last stage; stage 0, whose Y
+            // half is read now -- its X half was read in the last stage).  Y's
+            // last MFMA readers (the last stage's half 1) are past the pad and
+            // the minima.
+            static_for<M>([&](auto MM) {
+                constexpr int m = decltype(MM)::value;
+                ds_rd128<m * 2048>(Y[m], rd_addr + rd_h1);
+            });
+            if constexpr (ABL & 16)
+                asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" : "+v"(gr[0]), "+v"(gr[1])::"memory");
+            else
+                asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)\n\ts_barrier" : "+v"(gr[0]), "+v"(gr[1])::"memory");
+        } else {
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(gr[0]), "+v"(gr[1])::"memory");
+        }
         float tn[N];
-        tn[0] = qv0 ? min_raw(lr.tau[0], ord2f(gr[0])) : -FX_INF;
-        tn[1] = qv1 ? min_raw(lr.tau[1], ord2f(gr[1])) : -FX_INF;
+        // (a lane-mask select: the compiler had branched around min_raw)
+        tn[0] = __builtin_bit_cast(float, sel_mask(qm0, __builtin_bit_cast(uint32_t, -FX_INF),
+                                                   __builtin_bit_cast(uint32_t, min_raw(lr.tau[0], ord2f(gr[0])))));
+        tn[1] = __builtin_bit_cast(float, sel_mask(qm1, __builtin_bit_cast(uint32_t, -FX_INF),
+                                                   __builtin_bit_cast(uint32_t, min_raw(lr.tau[1], ord2f(gr[1])))));
         float mn[N];
 #pragma unroll
         for (int n = 0; n < N; ++n) mn[n] = min8_raw(gmin[n]);
@@ -518,9 +570,11 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
         if (q0 + q >= nq) break;
         const int cq = qi < 16 ? __builtin_amdgcn_readlane(lr.cnt[0], qi) : __builtin_amdgcn_readlane(lr.cnt[1], qi - 16);
         const int cn = min(cq, LCAP);
-        float d = lane < cn ? lst[q * LSTRIDE + lane] : FX_INF;
-        int i = lane < cn ? ((const int*)lst)[q * LSTRIDE + LCAP + lane] : INT_MAX;
-        sort64(d, i, lane);
+        uint32_t hi, lo;
+        load_packed(lst, (const int*)lst + LCAP, q * LSTRIDE + lane, lane < cn, hi, lo);
+        sort64_packed(hi, lo, lane);
+        const float d = ord2f(hi);
+        const int i = (int)lo;
         if (lane < KP) {
             p.cand_d[(obase + q) * KP + lane] = d;
             p.cand_i[(obase + q) * KP + lane] = i == INT_MAX ? -1 : i;
@@ -558,6 +612,7 @@ static hipError_t scan_v4_t(const ScanParams& p, hipStream_t s) {
             case 42: return scan_v4_t<DT, METRIC, KSTEPS, 42, LN>(p, s);
             case 58: return scan_v4_t<DT, METRIC, KSTEPS, 58, LN>(p, s);
             case 16: return scan_v4_t<DT, METRIC, KSTEPS, 16, LN>(p, s);
+            case 272: return scan_v4_t<DT, METRIC, KSTEPS, 272, LN>(p, s);
             case 64: return scan_v4_t<DT, METRIC, KSTEPS, 64, LN>(p, s);
             case 128: return scan_v4_t<DT, METRIC, KSTEPS, 128, LN>(p, s);
             case 192: return scan_v4_t<DT, METRIC, KSTEPS, 192, LN>(p, s);

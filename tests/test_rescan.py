@@ -90,9 +90,10 @@ def test_rescan_device_resident(diag_fx):
 
 
 def test_rescan_capacity_overflow(diag_fx):
-    """More flagged queries than the re-scan's capacity (RESCAN_MAX = 2048):
-    the first 2048 are re-scanned, the rest go straight to the exact scan
-    (k_rescan_overflow) -- every result exact, and the counts say so."""
+    """More flagged queries than the re-scan's chunk (RESCAN_MAX = 2048): the
+    re-scan runs in two chunks over the flagged list (k_rescan_chunks), so all
+    2,500 are re-scanned and certified and none goes to the exact scan --
+    every result exact, and the counts say so."""
     rng = np.random.default_rng(12)
     xb = rng.standard_normal((20_000, 64)).astype(np.float32)
     xq = rng.standard_normal((2500, 64)).astype(np.float32)
@@ -100,7 +101,7 @@ def test_rescan_capacity_overflow(diag_fx):
     ix.add(xb)
     ix.set_option("force_fallback", 1)
     D, I = ix.search(xq, 10)
-    assert ix.last_fallbacks() == 2500 and ix.last_exact_fallbacks() == 2500 - 2048
+    assert ix.last_fallbacks() == 2500 and ix.last_exact_fallbacks() == 0
     Dr, Ir = C.knn_exact(xq, xb, 10)
     assert_parity(D, I, Dr, Ir)
     ix.set_option("force_fallback", 0)

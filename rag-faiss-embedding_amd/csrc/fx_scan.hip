@@ -35,17 +35,24 @@
 
 #include <stdlib.h>
 
-// the epilogue's accumulator wait-state pad (acc_fence_v): 1 in the product;
-// 0 only in A/B builds (make OUT=... CXXFLAGS=-DFX_EPILOGUE_PAD=0)
+// The epilogue's accumulator wait-state pad (acc_fence_v) before the group
+// minima: 0 in the product (the minima read acc[0..7] in MFMA order, so the
+// last pairs' results are >= 28 VALU instructions old when read); 1 in A/B
+// builds (make variant V=pad VFLAGS=-DFX_EPILOGUE_PAD=1).  Same box, round 5
+// (profiles/r5/ab): without it (d) -1.0 %, the N = 8 shard -1.1 %, (b) -0.5 %;
+// in one ablation binary (e) -1.6 % at a 2.9 % lower in-kernel clock.
 #ifndef FX_EPILOGUE_PAD
-#define FX_EPILOGUE_PAD 1
+#define FX_EPILOGUE_PAD 0
 #endif
 // Each tile's first stage barrier taken at the end of the previous tile,
-// BEFORE its slow path, covering the next tile's stages 0 and 1 (1 in the
-// product; 0 in A/B builds: one barrier at the start of every stage).  See
-// the tile-end block in k_scan_v4.
+// BEFORE its slow path, covering the next tile's stages 0 and 1 (two stages
+// of slack for the partners of a wave in its slow path; see the tile-end
+// block in k_scan_v4).  Measured and off (profiles/r5/ab/r5c_sort_eb_pad.txt:
+// +1.2 % on (d), +1.0 % on the shard, +1.2 % on (b) against one barrier at
+// the start of every stage): the early wait for stage 2's pieces and the
+// Y(0) reads outside the MFMA shadow cost more than the slack saves.
 #ifndef FX_EARLY_BARRIER
-#define FX_EARLY_BARRIER 1
+#define FX_EARLY_BARRIER 0
 #endif
 
 namespace fx {
@@ -82,8 +89,9 @@ struct ScanLds {
 // issued as one burst after the first MFMA pair (results valid); 256 the
 // epilogue's fast path only (slow tiles counted into p.stamps, no pushes:
 // results invalid); 2048 no accumulator wait-state pad before the epilogue
-// (the round-4 variant; with 1024 for its slow-path stamps); 8192 the pad
-// twice (results valid: the power/clock A/B; with 1024: 9216)
+// (with 1024 for its slow-path stamps); 8192 one more pad (results valid: the
+// power/clock A/B; with 1024: 9216) -- since round 5 the product has no pad
+// (FX_EPILOGUE_PAD), so 2048 is the product and 8192 the round-4 epilogue
 //
 // LN selects the shape of the corpus LDS-DMA pieces and of the LDS image:
 //   LN = 0: fragment-shaped pieces (16 rows x 64 B: each piece touches 16

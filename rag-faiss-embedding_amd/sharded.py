@@ -125,12 +125,18 @@ class ShardedIndexFlatL2:
             return self.local.search(xq, k)
         host_in = not (isinstance(xq, torch.Tensor) and xq.is_cuda)
         if host_in and dist.get_backend(self.group) == "nccl":
-            is_np = not isinstance(xq, torch.Tensor)
-            xt = torch.from_numpy(np.ascontiguousarray(xq, dtype=np.float32)) if is_np else xq
-            dev = self.comm_device(xt)
-            D, I = self.local.search(xt.to(dev), k)
-            Dm, Im = self.exchange(D, I, k)
-            Dm, Im = Dm.cpu(), Im.cpu()
-            return (Dm.numpy(), Im.numpy()) if is_np else (Dm, Im)
+            return self.search_host_on_device(xq, k)
         D, I = self.local.search(xq, k)
         return self.exchange(D, I, k)
+
+    def search_host_on_device(self, xq, k: int):
+        """search() of host queries under RCCL: H2D of the queries, local
+        scan, all_gather and merge on the exchange device, ONE D2H of the
+        merged lists (numpy in -> numpy out, a host tensor -> host tensors)."""
+        is_np = not isinstance(xq, torch.Tensor)
+        xt = torch.from_numpy(np.ascontiguousarray(xq, dtype=np.float32)) if is_np else xq
+        dev = self.comm_device(xt)
+        D, I = self.local.search(xt.to(dev), k)
+        Dm, Im = self.exchange(D, I, k)
+        Dm, Im = Dm.cpu(), Im.cpu()
+        return (Dm.numpy(), Im.numpy()) if is_np else (Dm, Im)

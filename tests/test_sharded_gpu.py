@@ -95,7 +95,11 @@ def _rccl_worker(port, q):
         assert ix.comm_device(torch.from_numpy(D)) == torch.device("cuda", 0)
         Dm, Im = ix.exchange(D, I, k)            # real RCCL all_gather + fx_merge_shards
         Dr, Ir = C.knn_exact(xq, xb, k)
-        q.put((isinstance(Dm, np.ndarray), bool((Im == Ir).all()),
+        # the N > 1 host-query path (search() under nccl): H2D once, local scan,
+        # RCCL all_gather and merge on the device, one D2H
+        Dd, Id = ix.search_host_on_device(xq.astype(np.float64), k)
+        ok_dev = isinstance(Dd, np.ndarray) and bool((Id == Ir).all()) and bool((Dd == Dm).all())
+        q.put((isinstance(Dm, np.ndarray) and ok_dev, bool((Im == Ir).all()),
                bool((np.abs(Dm - Dr) <= 1e-5 * np.maximum(1.0, np.abs(Dr))).all())))
     except Exception as e:  # noqa: BLE001
         q.put((False, False, repr(e)))
@@ -106,7 +110,9 @@ def _rccl_worker(port, q):
 def test_exchange_under_rccl_host_inputs():
     """The exchange step under the nccl (RCCL) backend with the reference's
     host call form: numpy D / I from the local search are staged on the GPU,
-    gathered by RCCL and merged on the device, and come back as numpy
+    gathered by RCCL and merged on the device, and come back as numpy; and
+    the host-query search path of N > 1 (search_host_on_device: queries to the
+    GPU once, the whole exchange on the device, one D2H) gives the same lists
     (a world of 1: a one-GPU box cannot host two RCCL ranks)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

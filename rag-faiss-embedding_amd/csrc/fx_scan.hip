@@ -62,8 +62,13 @@ namespace fx {
 // waits instead of the mid-stage lgkmcnt(0), group minima beside the last
 // MFMAs, other DMA issue points and corpus pieces fused into the MFMA pair
 // before them were all no faster
+// FX_RING6 (A/B builds; needs FX_LCAP <= 48 to fit the LDS): 6 slots (5
+// stages in flight) for the instances with >= 5 stages per tile
+#ifndef FX_RING6
+#define FX_RING6 0
+#endif
 template <int KSTEPS>
-constexpr int ring_slots() { return 5; }
+constexpr int ring_slots() { return (FX_RING6 && KSTEPS >= 10) ? 6 : 5; }
 constexpr int S_STAGE = TILE_R * STAGE_B;       // 16 KiB = 128 rows x 128 B
 // norm / threshold slots first: every ring piece's LDS address is then >= 4 KiB,
 // more than any instruction offset subtracted from its M0 (see dma_piece)
@@ -287,8 +292,10 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
             // VMEM ops younger than stage g+1's: stages g+2 .. g+NS-2, issued
             // in the NS-3 stages before this one (4 corpus pieces each, + the
             // norm piece with a tile's first stage)
-            constexpr int W = 4 * (NS - 3) + ((j + 2) % SPT == 0) + ((j + 3) % SPT == 0);
-            static_assert(NS == 5, "wait count written for 5 slots");
+            constexpr int W = 4 * (NS - 3) + ((j + 2) % SPT == 0) + ((j + 3) % SPT == 0) +
+                              (NS >= 6 && (j + 4) % SPT == 0);
+            static_assert(NS == 5 || NS == 6, "wait count written for 5 or 6 slots");
+            static_assert(!EB || NS == 5, "the tile-end barrier's vmcnt is written for 5 slots");
             uint64_t s_a = 0, s_b = 0, s_c = 0;
             if constexpr (ABL & 64) {
                 s_a = __builtin_amdgcn_s_memtime();

@@ -13,8 +13,12 @@ namespace fx {
 // padding rows (|y|^2 = +inf -> key +inf) never do.
 constexpr float KEY_MAX = FLT_MAX;
 // k_scan_v4's per-query LDS list capacity (KP < LCAP <= 64, one sort64 lane
-// per entry; 56 entries with a 6-slot ring measured 1-2 % slower)
-constexpr int LCAP = 64;
+// per entry); 64 in the product, 48 in the 6-slot-ring A/B build (FX_RING6:
+// the lists then compact at 48 = capacity, entries past it wait in pend)
+#ifndef FX_LCAP
+#define FX_LCAP 64
+#endif
+constexpr int LCAP = FX_LCAP;
 static_assert(LCAP > KP && LCAP <= 64, "list capacity");
 // global-address-space float: loads through it are global_load (vmcnt only),
 // not flat (which also counts against lgkmcnt as a possible LDS access)

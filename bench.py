@@ -189,6 +189,31 @@ def oracle_corpus_chunks(args, n_total, d, dtype, device, rows=None):
         yield c0, x
 
 
+class Heartbeat:
+    """A stderr line every `period` s while a long silent leg runs (the
+    full-corpus recall oracle takes minutes): the GPU box's runner takes a
+    process that writes nothing for 3 minutes to be hung.  The oracle's C
+    calls release the GIL, so the thread gets to run."""
+
+    def __init__(self, what, period=30.0):
+        import threading
+        self.what, self.period, self.t0 = what, period, time.time()
+        self.stop = threading.Event()
+        self.th = threading.Thread(target=self.run, daemon=True)
+
+    def run(self):
+        while not self.stop.wait(self.period):
+            log(f"[bench] {self.what}: {time.time() - self.t0:.0f}s")
+
+    def __enter__(self):
+        self.th.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.stop.set()
+        self.th.join()
+
+
 def cpu_baseline_and_recall(args, n_total, d, dtype, k, D, I, xq_dev, nthreads, device):
     """cpu_baseline leg (rank 0): the repo's C/OpenMP restatement of FAISS's
     IndexFlatL2 BLAS path timed on a bounded sample of the same workload, and
@@ -529,7 +554,8 @@ def main():
             log("latency_nq1_f32 leg failed:", e)
     if rank == 0 and not args.no_cpu:
         nthreads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
-        extra = cpu_baseline_and_recall(args, n_total, d, dtype, k, D, I, xq, nthreads, device)
+        with Heartbeat("cpu leg (recall oracle, CPU baseline) running"):
+            extra = cpu_baseline_and_recall(args, n_total, d, dtype, k, D, I, xq, nthreads, device)
         if world > 1:
             extra.pop("cpu_baseline", None)
         out.update(extra)

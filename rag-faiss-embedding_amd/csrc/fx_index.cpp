@@ -96,6 +96,8 @@ struct Options {
     int compact_at = 0;      // FX_COMPACT_AT: list fill that triggers a compaction (0: default 48, KP < v <= CAP)
     int union_w = 0;         // FX_UNION_W: splits per union-bound window (16, 32, 64; 0: by split count)
     int union_defer = 1;     // FX_UNION_DEFER: union bounds fetched by LDS-DMA, bounded a tile later (0: in place)
+    int tight_at = -1;       // FX_TIGHT_AT: a list that took entries and holds >= this many gets its threshold
+                             // re-bounded without a compaction (-1 default, 0 off, KP < v <= CAP)
     int graph_verbose = 0;   // FX_SEARCH_GRAPH_VERBOSE
 #ifdef FX_DIAG
     int force_fallback = 0;  // FX_FORCE_FALLBACK: flag every query (1: -> re-scan, 2: -> exact scan)
@@ -123,6 +125,7 @@ struct Options {
         num("FX_COMPACT_AT", compact_at);
         num("FX_UNION_W", union_w);
         num("FX_UNION_DEFER", union_defer);
+        num("FX_TIGHT_AT", tight_at);
         num("FX_SEARCH_GRAPH_VERBOSE", graph_verbose);
         (void)str;
 #ifdef FX_DIAG
@@ -157,6 +160,7 @@ struct Options {
             {"compact_at", &compact_at, 0, CAP, nullptr, 0},
             {"union_w", &union_w, 0, 64, kWindows, 4},
             {"union_defer", &union_defer, 0, 1, nullptr, 0},
+            {"tight_at", &tight_at, -1, CAP, nullptr, 0},
 #ifdef FX_DIAG
             {"force_fallback", &force_fallback, 0, 2, nullptr, 0},
             {"scan_dbg", &scan_dbg, 0, 1 << 20, nullptr, 0},
@@ -171,6 +175,8 @@ struct Options {
             }
             // compact_at: 0 (default) or a fill in (KP, CAP]
             if (ok && sl.v == &compact_at) ok = value == 0 || value > KP;
+            // tight_at: -1 (default), 0 (off) or a fill in (KP, CAP]
+            if (ok && sl.v == &tight_at) ok = value <= 0 || value > KP;
             *why = ok ? nullptr : "value out of range";
             return sl.v;
         }
@@ -326,6 +332,8 @@ void plan_scan(const FxIndex* h, int64_t nq, int k, ScanParams& p) {
     p.share = k <= KP ? 1 : 0;
     p.union_w = 16;
     p.union_defer = h->opt.union_defer;
+    // list re-bounding between compactions (k <= KP only; -1: the default)
+    p.tight_at = p.share && h->opt.tight_at > KP ? h->opt.tight_at : 0;
     const int ntl = p.n_qtiles, nct = p.n_ctiles;
     constexpr int min_tiles = 4;
     // placement (map_tile): corpus-partitioned by default (config (d): 257 vs
@@ -895,7 +903,7 @@ std::vector<uint64_t> graph_key(const FxIndex* h, int64_t nq, int q_dtype, int k
             (uint64_t)h->img_kind, (uint64_t)h->centred, (uint64_t)h->img_rows,
             (uint64_t)o.force_fallback, (uint64_t)o.place, (uint64_t)o.sx, (uint64_t)o.reduce_cand,
             (uint64_t)o.pub, (uint64_t)o.prune_rank, (uint64_t)o.compact_at, (uint64_t)o.union_w,
-            (uint64_t)o.union_defer,
+            (uint64_t)o.union_defer, (uint64_t)(int64_t)o.tight_at,
             (uint64_t)(uintptr_t)h->codes, (uint64_t)(uintptr_t)h->norms, (uint64_t)(uintptr_t)h->split.p,
             (uint64_t)(uintptr_t)h->cnorms.p, (uint64_t)(uintptr_t)h->centre.p, (uint64_t)(uintptr_t)h->qshift.p,
             (uint64_t)(uintptr_t)h->qin.p, (uint64_t)(uintptr_t)h->qf32.p, (uint64_t)(uintptr_t)h->qop.p,

@@ -75,6 +75,8 @@ struct ScanParams {
                                 // count is min(*nq_dev, nq), known only on the device
     int union_defer;            // 1: a compaction's union bound is fetched by LDS-DMA and bounded at
                                 // the next tile's epilogue (compact_regs); 0: waited for in place
+    int tight_at;               // > 0: a list that took entries in a tile and holds >= tight_at (below
+                                // the compaction trigger) gets its threshold re-bounded (tighten_list)
 };
 
 // queries are zero-padded to a multiple of QPAD (the scan's query tile)

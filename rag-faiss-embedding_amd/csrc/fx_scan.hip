@@ -503,6 +503,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                             if (rl0 + 16 * m + i >= lim) acc[m][n][i] = FX_INF;
             }
             int rb = trow0 + rl0;  // row of acc[0][*][0] in this lane
+            const int cnt_in0 = lr.cnt[0], cnt_in1 = lr.cnt[1];  // (tight_at: which lists take entries)
             unsigned pend[N] = {0u, 0u};
             unsigned ovf = 0u;
             static_for<N>([&](auto NN) {
@@ -523,6 +524,20 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
             if constexpr (ABL & (64 | 1024)) stq[11] += __builtin_amdgcn_s_memtime() - s_sl;
             // compact every list that reached p.compact_at (and any that overflowed)
             const int cat = min(p.compact_at, LCAP);  // the plan's trigger, within this kernel's lists
+            if (p.tight_at > 0) {
+                // lists that took entries in this tile and hold tight_at or more,
+                // below the compaction trigger: re-bound their thresholds
+                const uint64_t t0 = __builtin_amdgcn_ballot_w64(lane < 16 && qv0 && lr.cnt[0] > cnt_in0 &&
+                                                                lr.cnt[0] >= p.tight_at && lr.cnt[0] < cat);
+                const uint64_t t1 = __builtin_amdgcn_ballot_w64(lane < 16 && qv1 && lr.cnt[1] > cnt_in1 &&
+                                                                lr.cnt[1] >= p.tight_at && lr.cnt[1] < cat);
+                uint64_t tl = (t0 & 0xffffull) | ((t1 & 0xffffull) << 16);
+                while (tl) {
+                    const int qi = __builtin_ctzll(tl);
+                    tl &= tl - 1;
+                    tighten_list(lst, lr, qi, qw0 + qi, p.prune_rank, p.share ? gtq : nullptr, lane);
+                }
+            }
             bool need = ovf != 0u || lr.cnt[0] >= cat || lr.cnt[1] >= cat;
             while (__builtin_expect(__builtin_amdgcn_ballot_w64(need) != 0, 0)) {
                 uint64_t s_cp = 0;
@@ -631,6 +646,17 @@ static hipError_t scan_v4_t(const ScanParams& p, hipStream_t s) {
             case 64: return scan_v4_t<DT, METRIC, KSTEPS, 64, LN>(p, s);
             case 128: return scan_v4_t<DT, METRIC, KSTEPS, 128, LN>(p, s);
             case 192: return scan_v4_t<DT, METRIC, KSTEPS, 192, LN>(p, s);
+            case 256: return scan_v4_t<DT, METRIC, KSTEPS, 256, LN>(p, s);
+            case 1024: return scan_v4_t<DT, METRIC, KSTEPS, 1024, LN>(p, s);
+            default: break;
+        }
+    }
+    // config (b)'s split-fp32 instance: phase stamps, slow-path stamps, and
+    // the fast-path / no-epilogue ceilings
+    if constexpr (ABL == 0 && METRIC == L2 && DT == F32S && KSTEPS == 24) {
+        switch (p.dbg & 16383) {
+            case 8: return scan_v4_t<DT, METRIC, KSTEPS, 8, LN>(p, s);
+            case 64: return scan_v4_t<DT, METRIC, KSTEPS, 64, LN>(p, s);
             case 256: return scan_v4_t<DT, METRIC, KSTEPS, 256, LN>(p, s);
             case 1024: return scan_v4_t<DT, METRIC, KSTEPS, 1024, LN>(p, s);
             default: break;

@@ -388,6 +388,40 @@ __device__ __forceinline__ ListRegs compact_regs(float* lst, ListRegs r, unsigne
     return r;
 }
 
+// Re-bound the pruning threshold of this wave's list qi (wave-local query
+// index) without compacting it (option tight_at): a bisection over the
+// ordered-uint keys of its cq <= LCAP entries for the smallest v with at
+// least `rank` entries <= v, starting from hi = the current threshold (which
+// already qualifies: after a compaction it is the kept list's rank-th key,
+// before one FLT_MAX).  Every entry is the key of a distinct row of this
+// split, so v bounds the split's rank-th key: a valid threshold, published to
+// the shared one too.  ~60 instructions per list against ~350 for a
+// compaction, so thresholds can follow the pushes closely (fewer record tiles)
+// while compactions happen only when a list is near full.
+__device__ __forceinline__ void tighten_list(const float* lst_d, ListRegs& r, int qi, int q, int rank, unsigned* gtq,
+                                             int lane) {
+    const int cq = __builtin_amdgcn_readlane(qi < 16 ? r.cnt[0] : r.cnt[1], qi & 15);
+    if (cq < rank) return;
+    const unsigned kv = lane < cq ? f2ord(lst_d[q * LSTRIDE + lane]) : 0xFFFFFFFFu;
+    unsigned hi = f2ord(readlane_f(qi < 16 ? r.tau[0] : r.tau[1], qi & 15));
+    unsigned lo = kv;
+    static_for<6>([&](auto T) {
+        const unsigned t = (unsigned)lane_xor<(32 >> decltype(T)::value)>((int)lo, lane);
+        lo = t < lo ? t : lo;
+    });
+    for (int it = 0; it < 8 && lo < hi; ++it) {
+        const unsigned mid = lo + (hi - lo) / 2;
+        if (__popcll(__builtin_amdgcn_ballot_w64(kv <= mid)) >= rank) hi = mid;
+        else lo = mid + 1;
+    }
+    const float v = ord2f(hi);
+    if ((lane & 15) == (qi & 15)) {
+        if (qi < 16) r.tau[0] = fminf(r.tau[0], v);
+        else r.tau[1] = fminf(r.tau[1], v);
+    }
+    if (gtq && lane == 0) gmin_u32(gtq + qi, hi);
+}
+
 // minima without fminf's operand canonicalisation (a v_max per operand: the
 // compiler cannot see that asm results are canonical)
 __device__ __forceinline__ float min_raw(float a, float b) {

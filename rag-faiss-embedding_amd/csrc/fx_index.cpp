@@ -98,6 +98,8 @@ struct Options {
     int union_defer = 1;     // FX_UNION_DEFER: union bounds fetched by LDS-DMA, bounded a tile later (0: in place)
     int tight_at = -1;       // FX_TIGHT_AT: a list that took entries and holds >= this many gets its threshold
                              // re-bounded without a compaction (-1 default, 0 off, KP < v <= CAP)
+    int cold_bound = 0;      // FX_COLD_BOUND: an empty list's first record tile bounds its threshold by the
+                             // rank-th of the tile's group minima before pushing (0 off, 1 on)
     int graph_verbose = 0;   // FX_SEARCH_GRAPH_VERBOSE
 #ifdef FX_DIAG
     int force_fallback = 0;  // FX_FORCE_FALLBACK: flag every query (1: -> re-scan, 2: -> exact scan)
@@ -126,6 +128,7 @@ struct Options {
         num("FX_UNION_W", union_w);
         num("FX_UNION_DEFER", union_defer);
         num("FX_TIGHT_AT", tight_at);
+        num("FX_COLD_BOUND", cold_bound);
         num("FX_SEARCH_GRAPH_VERBOSE", graph_verbose);
         (void)str;
 #ifdef FX_DIAG
@@ -161,6 +164,7 @@ struct Options {
             {"union_w", &union_w, 0, 64, kWindows, 4},
             {"union_defer", &union_defer, 0, 1, nullptr, 0},
             {"tight_at", &tight_at, -1, CAP, nullptr, 0},
+            {"cold_bound", &cold_bound, 0, 1, nullptr, 0},
 #ifdef FX_DIAG
             {"force_fallback", &force_fallback, 0, 2, nullptr, 0},
             {"scan_dbg", &scan_dbg, 0, 1 << 20, nullptr, 0},
@@ -334,6 +338,7 @@ void plan_scan(const FxIndex* h, int64_t nq, int k, ScanParams& p) {
     p.union_defer = h->opt.union_defer;
     // list re-bounding between compactions (k <= KP only; -1: the default)
     p.tight_at = p.share && h->opt.tight_at > KP ? h->opt.tight_at : 0;
+    p.cold_bound = p.share ? h->opt.cold_bound : 0;
     const int ntl = p.n_qtiles, nct = p.n_ctiles;
     constexpr int min_tiles = 4;
     // placement (map_tile): corpus-partitioned by default (config (d): 257 vs
@@ -903,7 +908,7 @@ std::vector<uint64_t> graph_key(const FxIndex* h, int64_t nq, int q_dtype, int k
             (uint64_t)h->img_kind, (uint64_t)h->centred, (uint64_t)h->img_rows,
             (uint64_t)o.force_fallback, (uint64_t)o.place, (uint64_t)o.sx, (uint64_t)o.reduce_cand,
             (uint64_t)o.pub, (uint64_t)o.prune_rank, (uint64_t)o.compact_at, (uint64_t)o.union_w,
-            (uint64_t)o.union_defer, (uint64_t)(int64_t)o.tight_at,
+            (uint64_t)o.union_defer, (uint64_t)(int64_t)o.tight_at, (uint64_t)o.cold_bound,
             (uint64_t)(uintptr_t)h->codes, (uint64_t)(uintptr_t)h->norms, (uint64_t)(uintptr_t)h->split.p,
             (uint64_t)(uintptr_t)h->cnorms.p, (uint64_t)(uintptr_t)h->centre.p, (uint64_t)(uintptr_t)h->qshift.p,
             (uint64_t)(uintptr_t)h->qin.p, (uint64_t)(uintptr_t)h->qf32.p, (uint64_t)(uintptr_t)h->qop.p,

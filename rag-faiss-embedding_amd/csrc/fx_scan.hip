@@ -502,6 +502,42 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                         for (int i = 0; i < 4; ++i)
                             if (rl0 + 16 * m + i >= lim) acc[m][n][i] = FX_INF;
             }
+            if (p.cold_bound) {
+                // An empty list (nothing pushed yet in this block: a split that
+                // starts cold pushes all 128 rows of its first tiles, overflows
+                // and compacts several times): bound its threshold first from
+                // the tile's group minima.  A lane's 8 group minima are keys of
+                // 8 distinct rows of its query, so with c = ceil(rank / 4) the
+                // largest over the query's 4 lanes of each lane's c-th smallest
+                // minimum has >= 4c >= rank rows at or below it: a valid bound
+                // on the split's rank-th key (rank <= 16).  Insertion into a
+                // per-lane (a1 <= a2 <= a3 <= a4) by v_med3, then a quad max.
+                // (rank read outside the lambda: a by-reference capture of p
+                // would put the kernel arguments in scratch)
+                const int c = (p.prune_rank + 3) >> 2;
+                static_for<N>([&](auto NN) {
+                    constexpr int n = decltype(NN)::value;
+                    const bool qv = n == 0 ? qv0 : qv1;
+                    if (c <= 4 && __builtin_amdgcn_ballot_w64(qv && lr.cnt[n] == 0 && mn[n] <= tn[n])) {
+                        float a1 = FX_INF, a2 = FX_INF, a3 = FX_INF, a4 = FX_INF;
+#pragma unroll
+                        for (int m = 0; m < M; ++m) {
+                            const float x = gmin[n][m];
+                            a4 = __builtin_amdgcn_fmed3f(a3, x, a4);
+                            a3 = __builtin_amdgcn_fmed3f(a2, x, a3);
+                            a2 = __builtin_amdgcn_fmed3f(a1, x, a2);
+                            a1 = fminf(a1, x);
+                        }
+                        float b = c <= 1 ? a1 : c == 2 ? a2 : c == 3 ? a3 : a4;
+                        b = fmaxf(b, lane_xor<16>(b, lane));
+                        b = fmaxf(b, lane_xor<32>(b, lane));
+                        if (qv && lr.cnt[n] == 0) {
+                            tn[n] = fminf(tn[n], b);
+                            lr.tau[n] = fminf(lr.tau[n], b);
+                        }
+                    }
+                });
+            }
             int rb = trow0 + rl0;  // row of acc[0][*][0] in this lane
             const int cnt_in0 = lr.cnt[0], cnt_in1 = lr.cnt[1];  // (tight_at: which lists take entries)
             unsigned pend[N] = {0u, 0u};

@@ -56,3 +56,18 @@ def test_checker_flags_known_hazards(tmp_path):
     r = subprocess.run([sys.executable, str(ROOT / "tools" / "check_dma_hazards.py"), str(s)],
                        capture_output=True, text=True)
     assert r.returncode == 1 and "2 hazard(s)" in r.stdout
+
+
+@pytest.mark.parametrize("unit", UNITS)
+def test_scan_kernels_use_no_scratch(asm_files, unit):
+    """Every k_scan_v4 instance runs without private (scratch) memory: its
+    stage waits count the VMEM operations in flight (`s_waitcnt vmcnt(N)` with
+    a compile-time N), and a scratch load or store would be one more such
+    operation the count does not know about.  (A by-reference lambda capture
+    of the kernel's by-value parameters once put them in scratch.)"""
+    import re
+    text = asm_files[unit].read_text()
+    sizes = re.findall(r"\.name:\s+(_ZN2fx9k_scan_v4\S+)\s+\.private_segment_fixed_size:\s+(\d+)", text)
+    assert sizes, "no k_scan_v4 kernel metadata found"
+    bad = [(n, int(v)) for n, v in sizes if int(v) != 0]
+    assert not bad, f"scan kernels with scratch: {bad}"

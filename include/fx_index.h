@@ -99,7 +99,10 @@ int fx_index_set_stream(FxIndex* index, void* stream);
  * "compact_at" 0 (= 48) or 33..64 (list fill that triggers a compaction), "union_w"
  * 0/16/32/64 (splits per union-bound window), "union_defer" 0/1 (default 1:
  * a compaction's union bound fetched by LDS-DMA and bounded a tile later
- * instead of waited for).  None changes results, only
+ * instead of waited for), "tight_at" -1/0 (off) or 33..64 (a list that took
+ * entries and holds at least this many gets its threshold re-bounded between
+ * compactions), "cold_bound" 0/1 (an empty list's first record tile bounds its
+ * threshold from the per-lane group minima).  None changes results, only
  * speed.  Unknown name or out-of-range value: FX_E_ARG.  (The diagnostic
  * build libfx_index_diag.so adds test hooks -- "force_fallback",
  * "scan_dbg" -- that the product library does not have.) */

@@ -99,7 +99,8 @@ struct Options {
     int tight_at = -1;       // FX_TIGHT_AT: a list that took entries and holds >= this many gets its threshold
                              // re-bounded without a compaction (-1 default, 0 off, KP < v <= CAP)
     int cold_bound = 0;      // FX_COLD_BOUND: an empty list's first record tile bounds its threshold by the
-                             // rank-th of the tile's group minima before pushing (0 off, 1 on)
+                             // rank-th of the tile's group minima before pushing (0 off, 1 on).  Both
+                             // measured slower and off (profiles/r5/ab/r5h_tight_cold.txt)
     int graph_verbose = 0;   // FX_SEARCH_GRAPH_VERBOSE
 #ifdef FX_DIAG
     int force_fallback = 0;  // FX_FORCE_FALLBACK: flag every query (1: -> re-scan, 2: -> exact scan)

@@ -101,8 +101,6 @@ struct Options {
     int cold_bound = 0;      // FX_COLD_BOUND: an empty list's first record tile bounds its threshold by the
                              // rank-th of the tile's group minima before pushing (0 off, 1 on).  Both
                              // measured slower and off (profiles/r5/ab/r5h_tight_cold.txt)
-    int pace = 0;            // FX_SCAN_PACE: two query tiles under placement 1 (nq in (128, 256]): a block
-                             // more than pace - 1 tiles ahead of its split's other block waits (0 off)
     int graph_verbose = 0;   // FX_SEARCH_GRAPH_VERBOSE
 #ifdef FX_DIAG
     int force_fallback = 0;  // FX_FORCE_FALLBACK: flag every query (1: -> re-scan, 2: -> exact scan)
@@ -132,7 +130,6 @@ struct Options {
         num("FX_UNION_DEFER", union_defer);
         num("FX_TIGHT_AT", tight_at);
         num("FX_COLD_BOUND", cold_bound);
-        num("FX_SCAN_PACE", pace);
         num("FX_SEARCH_GRAPH_VERBOSE", graph_verbose);
         (void)str;
 #ifdef FX_DIAG
@@ -169,7 +166,6 @@ struct Options {
             {"union_defer", &union_defer, 0, 1, nullptr, 0},
             {"tight_at", &tight_at, -1, CAP, nullptr, 0},
             {"cold_bound", &cold_bound, 0, 1, nullptr, 0},
-            {"scan_pace", &pace, 0, 8, nullptr, 0},
 #ifdef FX_DIAG
             {"force_fallback", &force_fallback, 0, 2, nullptr, 0},
             {"scan_dbg", &scan_dbg, 0, 1 << 20, nullptr, 0},
@@ -218,7 +214,7 @@ struct FxIndex {
     Options opt;
     // search workspace
     DevBuf qin, qf32, qop, qeps, qrho, cand_d, cand_i, cand2_d, cand2_i, dws, iws, flag, fbc_d, fbc_i, stage, gtau,
-        trace, dbgbuf, stamps, pub, pace;
+        trace, dbgbuf, stamps, pub;
     // the re-scan of uncertified queries (plan_rescan): its own query
     // operands, thresholds, candidate lists and flagged list
     DevBuf rq_f32, rq_op, rq_eps, rq_rho, rq_shift, rq_gtau, rq_cand_d, rq_cand_i, rq_flag;
@@ -344,8 +340,6 @@ void plan_scan(const FxIndex* h, int64_t nq, int k, ScanParams& p) {
     // list re-bounding between compactions (k <= KP only; -1: the default)
     p.tight_at = p.share && h->opt.tight_at > KP ? h->opt.tight_at : 0;
     p.cold_bound = p.share ? h->opt.cold_bound : 0;
-    p.pace = nullptr;  // plan_search
-    p.pace_w = 0;
     const int ntl = p.n_qtiles, nct = p.n_ctiles;
     constexpr int min_tiles = 4;
     // placement (map_tile): corpus-partitioned by default (config (d): 257 vs
@@ -607,13 +601,6 @@ hipError_t plan_search(FxIndex* h, int64_t nq, const void* qdev, int q_dtype, in
     sp.qop = (const char*)h->qop.p;
     sp.nq = nq;
     sp.dbg = h->opt.scan_dbg;
-    // pacing of the two blocks that stream one split (placement 1 with two
-    // query tiles): a progress word per block, zeroed before each scan
-    if (h->opt.pace > 0 && sp.place == 1 && sp.n_qtiles == 2) {
-        if ((e = h->pace.ensure((size_t)sp.splits * 2 * 4)) != hipSuccess) return e;
-        sp.pace = (int*)h->pace.p;
-        sp.pace_w = h->opt.pace - 1;
-    }
     if ((e = h->gtau.ensure((size_t)P.nq_pad * 4)) != hipSuccess) return e;
     sp.gtau = (unsigned*)h->gtau.p;
     // k_scan_v4's published per-split lists (the union threshold, see
@@ -693,7 +680,6 @@ hipError_t enqueue_search(FxIndex* h, SearchPlan& P, hipStream_t s, bool timed, 
         const size_t npub = (size_t)P.sp.n_qtiles * TILE_Q * P.sp.splits * KP;
         if ((e = hipMemsetD32Async((hipDeviceptr_t)P.sp.pub, 0x7f800000u, npub, s)) != hipSuccess) return e;  // +inf
     }
-    if (P.sp.pace && (e = hipMemsetAsync(P.sp.pace, 0, (size_t)P.sp.splits * 2 * 4, s)) != hipSuccess) return e;
     if (timed && (e = hipEventRecord(ev[0], s)) != hipSuccess) return e;
     if ((e = launch_scan(P.scan_dt, h->metric, P.sp, s)) != hipSuccess) return e;
     if (timed && (e = hipEventRecord(ev[1], s)) != hipSuccess) return e;
@@ -924,7 +910,7 @@ std::vector<uint64_t> graph_key(const FxIndex* h, int64_t nq, int q_dtype, int k
             (uint64_t)o.force_fallback, (uint64_t)o.place, (uint64_t)o.sx, (uint64_t)o.reduce_cand,
             (uint64_t)o.pub, (uint64_t)o.prune_rank, (uint64_t)o.compact_at, (uint64_t)o.union_w,
             (uint64_t)o.union_defer, (uint64_t)(int64_t)o.tight_at, (uint64_t)o.cold_bound,
-            (uint64_t)o.pace, (uint64_t)(uintptr_t)h->pace.p, (uint64_t)(uintptr_t)h->codes, (uint64_t)(uintptr_t)h->norms, (uint64_t)(uintptr_t)h->split.p,
+            (uint64_t)(uintptr_t)h->codes, (uint64_t)(uintptr_t)h->norms, (uint64_t)(uintptr_t)h->split.p,
             (uint64_t)(uintptr_t)h->cnorms.p, (uint64_t)(uintptr_t)h->centre.p, (uint64_t)(uintptr_t)h->qshift.p,
             (uint64_t)(uintptr_t)h->qin.p, (uint64_t)(uintptr_t)h->qf32.p, (uint64_t)(uintptr_t)h->qop.p,
             (uint64_t)(uintptr_t)h->qeps.p, (uint64_t)(uintptr_t)h->qrho.p, (uint64_t)(uintptr_t)h->gtau.p,
@@ -1100,7 +1086,7 @@ void fx_index_free(FxIndex* h) {
                           &h->fbc_d, &h->fbc_i, &h->stage, &h->gtau, &h->trace, &h->dbgbuf, &h->split, &h->cnorms,
                           &h->centre, &h->mu_part, &h->qshift, &h->qrho, &h->stamps, &h->pub, &h->cand2_d,
                           &h->cand2_i, &h->rq_f32, &h->rq_op, &h->rq_eps, &h->rq_rho, &h->rq_shift, &h->rq_gtau,
-                          &h->rq_cand_d, &h->rq_cand_i, &h->rq_flag, &h->hk_ws, &h->pace})
+                          &h->rq_cand_d, &h->rq_cand_i, &h->rq_flag, &h->hk_ws})
             b->release();
         graph_release(h);
         if (h->ghq) (void)hipHostFree(h->ghq);

@@ -79,10 +79,6 @@ struct ScanParams {
                                 // the compaction trigger) gets its threshold re-bounded (tighten_list)
     int cold_bound;             // 1: a still-empty list's first record tile bounds its threshold by the
                                 // prune_rank-th of the tile's group minima before pushing
-    int* pace;                  // non-null (two query tiles under placement 1): [splits][2] tiles each
-                                // block has finished; a block more than pace_w tiles ahead of the
-                                // other block of its split waits for it (bounded)
-    int pace_w;
 };
 
 // queries are zero-padded to a multiple of QPAD (the scan's query tile)

@@ -82,9 +82,7 @@ struct ScanLds {
     static constexpr int LST_OFF = UNION_OFF + 4 * 2 * 1024;  // [TILE_Q][LCAP keys | LCAP rows]
     // [4 waves][keys 64 lanes | rows 64 lanes]: sink of the branch-free push
     static constexpr int TRASH_OFF = LST_OFF + TILE_Q * LSTRIDE * 4;
-    // pacing (ScanParams.pace): the other block's progress word, LDS-DMA'd
-    static constexpr int PACE_OFF = TRASH_OFF + 4 * 2 * 256;
-    static constexpr int BYTES = PACE_OFF + 16;
+    static constexpr int BYTES = TRASH_OFF + 4 * 2 * 256;
     static_assert(BYTES <= 160 * 1024, "LDS budget");
 };
 
@@ -109,8 +107,7 @@ struct ScanLds {
 //           XOR-swizzled by (r & 7) -- the swizzle is applied to the SOURCE
 //           address (LDS-DMA writes lane-linearly), and the fragment reads
 //           undo it, conflict-free for both K halves.
-constexpr int RESCAN = 4096;
-constexpr int PACE_POLLS = 24;  // pacing: polls (each ~0.5 us) before a block stops pacing  // ABL bit naming the re-scan's instance (no code change)
+constexpr int RESCAN = 4096;  // ABL bit naming the re-scan's instance (no code change)
 
 template <int DT, int METRIC, int KSTEPS, int ABL = 0, int LN = 0>
 __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
@@ -151,14 +148,6 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
     lr.tau[0] = lr.tau[1] = KEY_MAX;
     unsigned* gtq = p.gtau + q0 + qw0;
     float* pubw = p.pub ? p.pub + (q0 + qw0) * p.splits * KP : nullptr;
-    // pacing (two query tiles under placement 1): wave 0 publishes the tiles
-    // this block has finished and holds the block while it is too far ahead
-    // of the other block of its split (the workgroup waits at the next stage
-    // barrier), so both stream the split through the XCD's L2 together
-    const bool pw = p.pace != nullptr && wave == 0;
-    bool pace_live = pw;
-    int* const pace_self = pw ? p.pace + 2 * split + (qtile & 1) : nullptr;
-    const int* const pace_other = pw ? p.pace + 2 * split + ((qtile & 1) ^ 1) : nullptr;
 
     // queries -> AGPRs (B fragments), settled once before the DMA ring starts
     bfrag_t b[KSTEPS][N];
@@ -634,39 +623,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
             }
             cb_nxt = sgpr_ptr(cb_nxt);
         }
-        if (pw) {
-            // The other block's progress as LDS-DMA'd at the end of tile t - 1
-            // (landed: the stage barriers of this tile waited for every older
-            // VMEM op), so in step it reads t; only a block clearly ahead polls
-            // the word itself, a bounded number of times (the other block may
-            // not be resident: pacing then stops for this block).  The store
-            // and the DMA below are two VMEM ops outside the counted ring: they
-            // can only make a later counted wait of wave 0 wait longer.
-            if (pace_live && t > 0) {
-                int prog;
-                asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)"
-                             : "=v"(prog)
-                             : "v"(lds_base + (uint32_t)LDS::PACE_OFF)
-                             : "memory");
-                prog = __builtin_amdgcn_readfirstlane(prog);
-                if (t + 1 - prog > p.pace_w + 1) {
-                    for (int it = 0;; ++it) {
-                        const int v = __builtin_amdgcn_readfirstlane(
-                            __hip_atomic_load(pace_other, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                        if (t + 1 - v <= p.pace_w) break;
-                        if (it == PACE_POLLS) {
-                            pace_live = false;
-                            break;
-                        }
-                        __builtin_amdgcn_s_sleep(8);
-                    }
-                }
-            }
-            __hip_atomic_store(pace_self, t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (pace_live) dma_word(pace_other, lds_base + (uint32_t)LDS::PACE_OFF);
-        }
     }
-    if (pw) __hip_atomic_store(pace_self, 1 << 30, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
     // retire the ring's look-ahead pieces: an LDS-DMA still in flight at exit
     // would land in the LDS of the next workgroup on this CU (a deferred union

@@ -70,19 +70,6 @@ __device__ __forceinline__ void dma_norm_piece(const char* vaddr, uint32_t m0) {
         : "v"(vaddr), "{m0}"(m0)
         : "memory");
 }
-// one dword (lane 0) into LDS at m0, read past the vector L1 (device scope)
-__device__ __forceinline__ void dma_word(const void* vaddr, uint32_t m0) {
-    uint64_t saved;
-    asm volatile(
-        "s_mov_b64 %0, exec\n\t"
-        "s_mov_b64 exec, 1\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dword %1, off sc1\n\t"
-        "s_mov_b64 exec, %0"
-        : "=&s"(saved)
-        : "v"(vaddr), "{m0}"(m0)
-        : "memory");
-}
 // LDS -> MFMA operand registers.  "+v": the destination keeps its register
 // for the whole kernel (no other value is ever placed there), so the only
 // writes to an operand register are these reads, scheduled >= 8 MFMAs after

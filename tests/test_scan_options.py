@@ -62,22 +62,3 @@ def test_compaction_and_union_options_exact(fx, kind, dtype, d):
         assert_parity(D, I, Dr, Ir)
         print(f"\n[scan-options] {kind} {dtype} compact_at={compact_at} union_w={union_w} "
               f"union_defer={defer} tight_at={tight} cold_bound={cold}: fallbacks {ix.last_fallbacks()}/{nq}")
-
-
-@pytest.mark.parametrize("nq", [256, 200])
-def test_pacing_exact(fx, nq):
-    """`scan_pace` (nq in (128, 256]: the two blocks of a split stream it
-    together, the one ahead waiting for the other, bounded) only changes
-    timing: results equal the oracle's for every allowed lag, including the
-    partial second query tile (nq = 200)."""
-    n, d, k = 300_000, 256, 10
-    xb = rows("clustered", n, d, 21)
-    xq = rows("clustered", nq, d, 22)
-    ix = fx.IndexFlatL2(d, dtype="bfloat16")
-    ix.add(xb)
-    Dr, Ir = C.knn_exact(xq, ix.reconstruct_n(0, n), k)
-    for pace in (1, 2, 4, 0):
-        ix.set_option("scan_pace", pace)
-        D, I = ix.search(xq, k)
-        assert_parity(D, I, Dr, Ir)
-        print(f"\n[scan-pace] nq={nq} pace={pace}: fallbacks {ix.last_fallbacks()}/{nq}")

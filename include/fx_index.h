@@ -101,8 +101,9 @@ int fx_index_set_stream(FxIndex* index, void* stream);
  * a compaction's union bound fetched by LDS-DMA and bounded a tile later
  * instead of waited for), "tight_at" -1/0 (off) or 33..64 (a list that took
  * entries and holds at least this many gets its threshold re-bounded between
- * compactions), "cold_bound" 0/1 (an empty list's first record tile bounds its
- * threshold from the per-lane group minima).  None changes results, only
+ * compactions), "cold_bound" -1/0/1 (an empty list's first record tile bounds its
+ * threshold from the per-lane group minima; -1, the default: on for corpus
+ * splits of <= 256 tiles).  None changes results, only
  * speed.  Unknown name or out-of-range value: FX_E_ARG.  (The diagnostic
  * build libfx_index_diag.so adds test hooks -- "force_fallback",
  * "scan_dbg" -- that the product library does not have.) */

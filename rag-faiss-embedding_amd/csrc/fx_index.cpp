@@ -98,9 +98,12 @@ struct Options {
     int union_defer = 1;     // FX_UNION_DEFER: union bounds fetched by LDS-DMA, bounded a tile later (0: in place)
     int tight_at = -1;       // FX_TIGHT_AT: a list that took entries and holds >= this many gets its threshold
                              // re-bounded without a compaction (-1 default, 0 off, KP < v <= CAP)
-    int cold_bound = 0;      // FX_COLD_BOUND: an empty list's first record tile bounds its threshold by the
-                             // rank-th of the tile's group minima before pushing (0 off, 1 on).  Both
-                             // measured slower and off (profiles/r5/ab/r5h_tight_cold.txt)
+    int cold_bound = -1;     // FX_COLD_BOUND: an empty list's first record tile bounds its threshold by the
+                             // rank-th of the tile's group minima before pushing (0 off, 1 on, -1: on for
+                             // splits of <= 256 tiles).  tight_at measured slower and off
+                             // (profiles/r5/ab/r5h_tight_cold.txt); cold_bound -1.8 % on (b), -1 % on (d)
+                             // at nq = 256 (short splits), +0.5-0.9 % on the long splits of (d) and the
+                             // N = 8 shard (r5h, r5i, r5k)
     int graph_verbose = 0;   // FX_SEARCH_GRAPH_VERBOSE
 #ifdef FX_DIAG
     int force_fallback = 0;  // FX_FORCE_FALLBACK: flag every query (1: -> re-scan, 2: -> exact scan)
@@ -165,7 +168,7 @@ struct Options {
             {"union_w", &union_w, 0, 64, kWindows, 4},
             {"union_defer", &union_defer, 0, 1, nullptr, 0},
             {"tight_at", &tight_at, -1, CAP, nullptr, 0},
-            {"cold_bound", &cold_bound, 0, 1, nullptr, 0},
+            {"cold_bound", &cold_bound, -1, 1, nullptr, 0},
 #ifdef FX_DIAG
             {"force_fallback", &force_fallback, 0, 2, nullptr, 0},
             {"scan_dbg", &scan_dbg, 0, 1 << 20, nullptr, 0},
@@ -339,7 +342,7 @@ void plan_scan(const FxIndex* h, int64_t nq, int k, ScanParams& p) {
     p.union_defer = h->opt.union_defer;
     // list re-bounding between compactions (k <= KP only; -1: the default)
     p.tight_at = p.share && h->opt.tight_at > KP ? h->opt.tight_at : 0;
-    p.cold_bound = p.share ? h->opt.cold_bound : 0;
+    p.cold_bound = 0;  // below, once the split count is known
     const int ntl = p.n_qtiles, nct = p.n_ctiles;
     constexpr int min_tiles = 4;
     // placement (map_tile): corpus-partitioned by default (config (d): 257 vs
@@ -379,6 +382,10 @@ void plan_scan(const FxIndex* h, int64_t nq, int k, ScanParams& p) {
     // 64, each contributing its first 256 / window published keys
     const int uw = h->opt.union_w;
     p.union_w = uw == 16 || uw == 32 || uw == 64 ? uw : p.splits <= 16 ? 16 : p.splits <= 32 ? 32 : 64;
+    // cold-start bound: pays on short splits, where a block's first record
+    // tiles are a large share of its work
+    const int cb = h->opt.cold_bound;
+    p.cold_bound = !p.share ? 0 : cb >= 0 ? cb : (nct + p.splits - 1) / p.splits <= 256 ? 1 : 0;
 }
 
 // k > KP: approx candidates the refine re-ranks exactly (k_refine_big)

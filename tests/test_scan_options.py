@@ -52,7 +52,7 @@ def test_compaction_and_union_options_exact(fx, kind, dtype, d):
     for compact_at, union_w, defer, tight, cold in [
             (64, 16, 1, 0, 0), (40, 16, 0, 0, 0), (48, 64, 1, 0, 0), (33, 32, 0, 0, 0), (64, 64, 0, 0, 0),
             (0, 0, 0, 0, 0), (0, 0, 1, 0, 0), (64, 16, 1, 33, 0), (48, 0, 1, 36, 1), (64, 64, 0, 40, 1),
-            (0, 0, 1, 0, 1), (0, 0, 1, -1, 0)]:
+            (0, 0, 1, 0, 1), (0, 0, 1, -1, -1)]:
         ix.set_option("compact_at", compact_at)
         ix.set_option("union_w", union_w)
         ix.set_option("union_defer", defer)

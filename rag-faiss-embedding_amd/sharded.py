@@ -139,4 +139,18 @@ class ShardedIndexFlatL2:
         D, I = self.local.search(xt.to(dev), k)
         Dm, Im = self.exchange(D, I, k)
         Dm, Im = Dm.cpu(), Im.cpu()
+        self._check_integrity()
         return (Dm.numpy(), Im.numpy()) if is_np else (Dm, Im)
+
+    def _check_integrity(self):
+        """A host-output search fails when the local scan's candidate lists
+        held row ids outside [0, ntotal), as the single-index host search does
+        (FX_E_INTEGRITY, fx_index.h): the local search here ran with device
+        outputs (stream-ordered), so its dropped count is read after the D2H
+        above has synchronised.  Device-output callers read
+        ``local.last_dropped_candidates()`` themselves (INTEGRATION.md)."""
+        dropped = getattr(self.local, "last_dropped_candidates", None)
+        if dropped is not None and dropped() > 0:
+            from ._lib import FxError
+            raise FxError(f"local search dropped {dropped()} corrupted candidate ids: its top-k may be "
+                          "missing rows")

@@ -181,3 +181,35 @@ def test_host_queries_under_rccl_stay_on_the_device(monkeypatch):
     # rank 1's lists are rank 0's with ids + 1000 (the fake gather): ties at
     # equal distance keep the smaller id
     assert (I[:, 0] == Ir[:, 0]).all() and (D[:, 0] == Dr[:, 0]).all()
+
+
+def test_host_queries_under_rccl_fail_on_dropped_candidates(monkeypatch):
+    """The sharded host-in path reports a corrupted local scan (candidate ids
+    outside [0, ntotal)) as an error, like the single-index host search's
+    FX_E_INTEGRITY, instead of returning a thinner top-k."""
+    from rag_faiss_embedding_amd._lib import FxError
+    from rag_faiss_embedding_amd.sharded import ShardedIndexFlatL2
+    monkeypatch.setattr(dist, "is_initialized", lambda: True)
+    monkeypatch.setattr(dist, "get_world_size", lambda g=None: 2)
+    monkeypatch.setattr(dist, "get_rank", lambda g=None: 0)
+    monkeypatch.setattr(dist, "get_backend", lambda g=None: "nccl")
+    monkeypatch.setattr(ShardedIndexFlatL2, "comm_device", lambda self, like: torch.device("cpu"))
+
+    class _BadShard(_OracleShard):
+        def search(self, xq, k):
+            D, I = super().search(xq.numpy(), k)
+            return torch.from_numpy(D), torch.from_numpy(I)
+
+        def last_dropped_candidates(self):
+            return 3
+
+    def merge(Dg, Ig, k):
+        Dm, Im = F.merge_topk(list(Dg.numpy()), list(Ig.numpy()), k)
+        return torch.from_numpy(Dm), torch.from_numpy(Im)
+
+    rng = np.random.default_rng(4)
+    ix = ShardedIndexFlatL2(8, 100, local_index=_BadShard(8, 0), merge_fn=merge)
+    ix.add(rng.standard_normal((50, 8)).astype(np.float32))
+    monkeypatch.setattr(dist, "all_gather_into_tensor", _fake_gather([], 2))
+    with pytest.raises(FxError, match="dropped 3"):
+        ix.search(rng.standard_normal((4, 8)).astype(np.float32), 5)

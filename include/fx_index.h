@@ -93,8 +93,8 @@ int fx_index_set_stream(FxIndex* index, void* stream);
 /* Per-index tuning option (name -> integer value).  Initial
  * values come from the FX_* environment variables, read once at index
  * creation; nothing on the search path reads the environment.  Names and
- * accepted values: "search_graph" 0/1 (replay small host searches as one
- * hipGraph), "scan_place" -1/0/1, "scan_sx" >= 0, "reduce_cand" 0/1,
+ * accepted values: "search_graph" 0/1 (default 1: replay small host searches
+ * as one hipGraph), "scan_place" -1/0/1, "scan_sx" >= 0, "reduce_cand" 0/1,
  * "f32_split" 0/1, "centre" 0/1, "scan_pub" 0/1, "prune_rank" 0..32,
  * "compact_at" 0 (= 48) or 33..64 (list fill that triggers a compaction), "union_w"
  * 0/16/32/64 (splits per union-bound window), "union_defer" 0/1 (default 1:

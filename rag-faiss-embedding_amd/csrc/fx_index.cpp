@@ -85,7 +85,8 @@ inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 // Test hooks and diagnostic dumps exist only in the diagnostic build
 // (-DFX_DIAG: libfx_index_diag.so, make diag / abl), never in libfx_index.so.
 struct Options {
-    int search_graph = 0;    // FX_SEARCH_GRAPH: replay small host searches as one hipGraph
+    int search_graph = 1;    // FX_SEARCH_GRAPH: replay small host searches as one hipGraph (round 5:
+                             // on by default, one-query call -7 % on a 100k x 384 fp32 index, r5r)
     int place = -1;          // FX_SCAN_PLACE: scan block placement (-1 automatic, 0, 1)
     int sx = 0;              // FX_SCAN_SX: corpus splits per XCD under placement 1 (0 automatic)
     int reduce_cand = 1;     // FX_REDUCE_CAND: merge 16 splits' lists before the refine (small nq)
@@ -679,10 +680,14 @@ hipError_t plan_search(FxIndex* h, int64_t nq, const void* qdev, int q_dtype, in
 // synchronisation: the same sequence is what a search graph captures.
 hipError_t enqueue_search(FxIndex* h, SearchPlan& P, hipStream_t s, bool timed, hipEvent_t* ev) {
     hipError_t e;
-    if ((e = launch_prep_queries(P.pp, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(P.rp.n_drop, 0, 4, s)) != hipSuccess) return e;
-    if ((e = hipMemsetD32Async((hipDeviceptr_t)P.sp.gtau, 0xff800000u, (size_t)P.nq_pad, s)) != hipSuccess)
-        return e;  // ord(+inf)
+    // the query preparation also resets the shared thresholds (ord(+inf)) and
+    // the dropped / flagged / exact counters (one kernel instead of memsets)
+    PrepParams pp1 = P.pp;
+    pp1.gtau = P.sp.gtau;
+    pp1.zero[0] = P.rp.n_drop;
+    pp1.zero[1] = P.rp.n_flag;
+    pp1.zero[2] = P.n_exact;
+    if ((e = launch_prep_queries(pp1, s)) != hipSuccess) return e;
     if (P.sp.pub) {
         const size_t npub = (size_t)P.sp.n_qtiles * TILE_Q * P.sp.splits * KP;
         if ((e = hipMemsetD32Async((hipDeviceptr_t)P.sp.pub, 0x7f800000u, npub, s)) != hipSuccess) return e;  // +inf
@@ -690,7 +695,6 @@ hipError_t enqueue_search(FxIndex* h, SearchPlan& P, hipStream_t s, bool timed, 
     if (timed && (e = hipEventRecord(ev[0], s)) != hipSuccess) return e;
     if ((e = launch_scan(P.scan_dt, h->metric, P.sp, s)) != hipSuccess) return e;
     if (timed && (e = hipEventRecord(ev[1], s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(P.rp.n_flag, 0, 4, s)) != hipSuccess) return e;
     RefineParams rp = P.rp;
     if (P.reduce) {
         int ng = 0;
@@ -713,20 +717,19 @@ hipError_t enqueue_search(FxIndex* h, SearchPlan& P, hipStream_t s, bool timed, 
     if ((P.sp.dbg & ~32) != 0) return hipSuccess;  // ablated scans: results invalid, no fallback chain
 #endif
     if ((e = launch_rescan_chunks(P.rp.n_flag, (int)RESCAN_MAX, P.nchunks, P.chunk_cnt, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(P.n_exact, 0, 4, s)) != hipSuccess) return e;
     for (int c = 0; c < P.nchunks; ++c) {  // chunk c: flagged queries [c RESCAN_MAX, ...)
         const int* list = P.rp.flag_list + (size_t)c * RESCAN_MAX;
         PrepParams pp = P.pp2;
         pp.qidx = list;
         pp.nq_dev = P.chunk_cnt + c;
+        pp.zero[0] = pp.zero[1] = pp.zero[2] = nullptr;
         ScanParams sp = P.sp2;
+        pp.gtau = sp.gtau;  // reset by the chunk's query preparation
         sp.nq_dev = P.chunk_cnt + c;
         RefineParams rp2 = P.rp2;
         rp2.nq_dev = P.chunk_cnt + c;
         rp2.out_idx = list;
         if ((e = launch_prep_queries(pp, s)) != hipSuccess) return e;
-        if ((e = hipMemsetD32Async((hipDeviceptr_t)sp.gtau, 0xff800000u, (size_t)pp.nq_pad, s)) != hipSuccess)
-            return e;
         if ((e = launch_scan(P.scan_dt, h->metric, sp, s)) != hipSuccess) return e;
         if ((e = launch_refine(h->dtype, h->metric, rp2, s)) != hipSuccess) return e;
     }

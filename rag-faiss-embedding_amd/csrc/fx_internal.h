@@ -163,6 +163,9 @@ struct PrepParams {
     const float* mu;        // centre of the scan image (null: none)
     const int* qidx;        // non-null: row r of the batch is row qidx[r] of q (the re-scan's gather)
     const int* nq_dev;      // non-null: live query count min(*nq_dev, nq); later rows are padding
+    // the search's resets, folded into this first kernel instead of memsets:
+    unsigned* gtau;         // non-null: [nq_pad] the scan's shared thresholds, set to ord(+inf)
+    int* zero[3];           // non-null entries: counters set to 0 (dropped ids, flagged, exact)
 };
 hipError_t launch_prep_queries(const PrepParams& p, hipStream_t s);
 hipError_t launch_scan(int st_dt, int metric, const ScanParams& p, hipStream_t s);

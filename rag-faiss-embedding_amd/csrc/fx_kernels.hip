@@ -459,6 +459,12 @@ __global__ __launch_bounds__(256) void k_prep_queries(PrepParams p, double gamma
     const int lane = threadIdx.x & 63;
     const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (r >= p.nq_pad) return;
+    if (lane == 0) {
+        if (p.gtau) p.gtau[r] = 0xff800000u;  // f2ord(+inf)
+        if (r == 0)
+            for (int i = 0; i < 3; ++i)
+                if (p.zero[i]) *p.zero[i] = 0;
+    }
     const int64_t nq = p.nq_dev ? min((int64_t)*p.nq_dev, p.nq) : p.nq;
     const bool live = r < nq;
     const int64_t src = live && p.qidx ? (int64_t)p.qidx[r] : r;  // source row of q

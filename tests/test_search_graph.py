@@ -23,6 +23,24 @@ def fx():
     return faiss
 
 
+def test_eager_small_search_equals_graph(fx, monkeypatch):
+    """search_graph is on by default: the eager path (FX_SEARCH_GRAPH=0)
+    stays covered and returns the replay's results exactly."""
+    rng = np.random.default_rng(12)
+    xb = rng.standard_normal((10_000, 384)).astype(np.float32)
+    q = rng.standard_normal((3, 384)).astype(np.float32)
+    out = {}
+    for g in ("0", "1"):
+        monkeypatch.setenv("FX_SEARCH_GRAPH", g)
+        ix = fx.IndexFlatL2(384)
+        ix.add(xb)
+        out[g] = [ix.search(q[i:i + 1], 5) for i in range(3)] + [ix.search(q, 5)]
+    Dr, Ir = C.knn_exact(q, xb, 5)
+    assert_parity(out["1"][3][0], out["1"][3][1], Dr, Ir)
+    for (De, Ie), (Dg, Ig) in zip(out["0"], out["1"]):
+        assert np.array_equal(Ie, Ig) and np.array_equal(De, Dg)
+
+
 def test_graph_replay_matches_oracle(fx, monkeypatch):
     monkeypatch.setenv("FX_SEARCH_GRAPH", "1")
     rng = np.random.default_rng(11)

@@ -99,7 +99,9 @@ int fx_index_set_stream(FxIndex* index, void* stream);
  * "compact_at" 0 (= 48) or 33..64 (list fill that triggers a compaction), "union_w"
  * 0/16/32/64 (splits per union-bound window), "union_defer" 0/1 (default 1:
  * a compaction's union bound fetched by LDS-DMA and bounded a tile later
- * instead of waited for), "tight_at" -1/0 (off) or 33..64 (a list that took
+ * instead of waited for), "union_inplace" -1..64 (lists per compaction
+ * bounded by the union in place beyond the deferred ones; -1, the default:
+ * 0 with union_defer, all without), "tight_at" -1/0 (off) or 33..64 (a list that took
  * entries and holds at least this many gets its threshold re-bounded between
  * compactions), "cold_bound" -1/0/1 (an empty list's first record tile bounds its
  * threshold from the per-lane group minima; -1, the default: on for corpus

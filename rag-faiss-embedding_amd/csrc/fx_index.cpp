@@ -97,6 +97,9 @@ struct Options {
     int compact_at = 0;      // FX_COMPACT_AT: list fill that triggers a compaction (0: default 48, KP < v <= CAP)
     int union_w = 0;         // FX_UNION_W: splits per union-bound window (16, 32, 64; 0: by split count)
     int union_defer = 1;     // FX_UNION_DEFER: union bounds fetched by LDS-DMA, bounded a tile later (0: in place)
+    int union_inplace = -1;  // FX_UNION_INPLACE: most lists per compaction call bounded in place beyond the
+                             // deferred ones (-1: 0 with union_defer, all without; r5v: 0 is -1.4 % on the
+                             // N = 8 shard and (b), (d) unchanged)
     int tight_at = -1;       // FX_TIGHT_AT: a list that took entries and holds >= this many gets its threshold
                              // re-bounded without a compaction (-1 default, 0 off, KP < v <= CAP)
     int cold_bound = -1;     // FX_COLD_BOUND: an empty list's first record tile bounds its threshold by the
@@ -132,6 +135,7 @@ struct Options {
         num("FX_COMPACT_AT", compact_at);
         num("FX_UNION_W", union_w);
         num("FX_UNION_DEFER", union_defer);
+        num("FX_UNION_INPLACE", union_inplace);
         num("FX_TIGHT_AT", tight_at);
         num("FX_COLD_BOUND", cold_bound);
         num("FX_SEARCH_GRAPH_VERBOSE", graph_verbose);
@@ -168,6 +172,7 @@ struct Options {
             {"compact_at", &compact_at, 0, CAP, nullptr, 0},
             {"union_w", &union_w, 0, 64, kWindows, 4},
             {"union_defer", &union_defer, 0, 1, nullptr, 0},
+            {"union_inplace", &union_inplace, -1, 64, nullptr, 0},
             {"tight_at", &tight_at, -1, CAP, nullptr, 0},
             {"cold_bound", &cold_bound, -1, 1, nullptr, 0},
 #ifdef FX_DIAG
@@ -341,6 +346,7 @@ void plan_scan(const FxIndex* h, int64_t nq, int k, ScanParams& p) {
     p.share = k <= KP ? 1 : 0;
     p.union_w = 16;
     p.union_defer = h->opt.union_defer;
+    p.union_inplace = h->opt.union_inplace >= 0 ? h->opt.union_inplace : p.union_defer ? 0 : (1 << 30);
     // list re-bounding between compactions (k <= KP only; -1: the default)
     p.tight_at = p.share && h->opt.tight_at > KP ? h->opt.tight_at : 0;
     p.cold_bound = 0;  // below, once the split count is known
@@ -919,7 +925,7 @@ std::vector<uint64_t> graph_key(const FxIndex* h, int64_t nq, int q_dtype, int k
             (uint64_t)h->img_kind, (uint64_t)h->centred, (uint64_t)h->img_rows,
             (uint64_t)o.force_fallback, (uint64_t)o.place, (uint64_t)o.sx, (uint64_t)o.reduce_cand,
             (uint64_t)o.pub, (uint64_t)o.prune_rank, (uint64_t)o.compact_at, (uint64_t)o.union_w,
-            (uint64_t)o.union_defer, (uint64_t)(int64_t)o.tight_at, (uint64_t)o.cold_bound,
+            (uint64_t)o.union_defer, (uint64_t)(int64_t)o.union_inplace, (uint64_t)(int64_t)o.tight_at, (uint64_t)o.cold_bound,
             (uint64_t)(uintptr_t)h->codes, (uint64_t)(uintptr_t)h->norms, (uint64_t)(uintptr_t)h->split.p,
             (uint64_t)(uintptr_t)h->cnorms.p, (uint64_t)(uintptr_t)h->centre.p, (uint64_t)(uintptr_t)h->qshift.p,
             (uint64_t)(uintptr_t)h->qin.p, (uint64_t)(uintptr_t)h->qf32.p, (uint64_t)(uintptr_t)h->qop.p,

@@ -77,6 +77,8 @@ struct ScanParams {
                                 // the next tile's epilogue (compact_regs); 0: waited for in place
     int tight_at;               // > 0: a list that took entries in a tile and holds >= tight_at (below
                                 // the compaction trigger) gets its threshold re-bounded (tighten_list)
+    int union_inplace;          // most lists per compaction call bounded in place by the union (those
+                                // past the deferred slots); the rest publish only their own bound
     int cold_bound;             // 1: a still-empty list's first record tile bounds its threshold by the
                                 // prune_rank-th of the tile's group minima before pushing
 };

@@ -579,7 +579,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                 uint64_t s_cp = 0;
                 if constexpr (ABL & (64 | 1024)) s_cp = __builtin_amdgcn_s_memtime();
                 lr = compact_regs(lst, lr, p.share ? gtq : nullptr, qw0, lane, p.pub ? pubw : nullptr, p.splits, split,
-                                  p.prune_rank, cat, p.union_w, upq, uslot, p.union_defer);
+                                  p.prune_rank, cat, p.union_w, upq, uslot, p.union_defer, p.union_inplace);
                 if constexpr (ABL & (64 | 1024)) {
                     stq[8] += 1;
                     stq[9] += __builtin_amdgcn_s_memtime() - s_cp;

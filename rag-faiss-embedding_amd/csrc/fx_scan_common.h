@@ -286,7 +286,7 @@ __device__ __forceinline__ void union_finish(int (&upq)[2], const float* uslot, 
 }
 __device__ __forceinline__ ListRegs compact_regs(float* lst, ListRegs r, unsigned* gtq, int qw0, int lane,
                                               float* pub, int splits, int split, int rank, int at, int uw,
-                                              int (&upq)[2], float* uslot, int defer) {
+                                              int (&upq)[2], float* uslot, int defer, int inplace_max) {
     float* lst_d = lst;                // keys of query q at q * LSTRIDE
     int* lst_i = (int*)(lst + LCAP);   // rows of query q at q * LSTRIDE
     int (&cntv)[2] = r.cnt;
@@ -347,8 +347,10 @@ __device__ __forceinline__ ListRegs compact_regs(float* lst, ListRegs r, unsigne
         dma_piece<0, 4>(voff, wb, lds_off(uslot + u * 256));  // s_nop 4: wb was written by VALU
         upq[u] = qi;
     }
-    // the rest now, up to 4 lists per memory round trip
-    while (rest) {
+    // the rest now, up to 4 lists per memory round trip (at most inplace_max
+    // lists: the others keep their own published bound until a later
+    // compaction; the union only prunes)
+    for (int done = 0; rest && done < inplace_max; done += 4) {
         int qs[4];
         unsigned kv[4][4];
 #pragma unroll

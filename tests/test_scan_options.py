@@ -6,7 +6,9 @@ its first 256 / union_w published keys), and whether a compaction's union
 bound is waited for in place or fetched by LDS-DMA and bounded a tile later
 (`union_defer`), and the re-bounding of a list's threshold between
 compactions (`tight_at`: a bisection over the list's keys for its rank-th),
-and an empty list's first bound from the tile's group minima (`cold_bound`).
+and an empty list's first bound from the tile's group minima (`cold_bound`),
+and how many lists of one compaction call take the union bound in place
+(`union_inplace`).
 All only change how fast the
 pruning threshold falls; every dropped row still lies above the final shared
 threshold that the refine certifies against.  Checked against the oracle on
@@ -49,16 +51,17 @@ def test_compaction_and_union_options_exact(fx, kind, dtype, d):
     ix.add(xb)
     ref = xb if dtype == "float32" else ix.reconstruct_n(0, n)
     Dr, Ir = C.knn_exact(xq, ref, k)
-    for compact_at, union_w, defer, tight, cold in [
-            (64, 16, 1, 0, 0), (40, 16, 0, 0, 0), (48, 64, 1, 0, 0), (33, 32, 0, 0, 0), (64, 64, 0, 0, 0),
-            (0, 0, 0, 0, 0), (0, 0, 1, 0, 0), (64, 16, 1, 33, 0), (48, 0, 1, 36, 1), (64, 64, 0, 40, 1),
-            (0, 0, 1, 0, 1), (0, 0, 1, -1, -1)]:
+    for compact_at, union_w, defer, tight, cold, inplace in [
+            (64, 16, 1, 0, 0, -1), (40, 16, 0, 0, 0, -1), (48, 64, 1, 0, 0, 64), (33, 32, 0, 0, 0, 4),
+            (64, 64, 0, 0, 0, 0), (0, 0, 0, 0, 0, -1), (0, 0, 1, 0, 0, 8), (64, 16, 1, 33, 0, -1),
+            (48, 0, 1, 36, 1, 64), (64, 64, 0, 40, 1, -1), (0, 0, 1, 0, 1, 0), (0, 0, 1, -1, -1, -1)]:
         ix.set_option("compact_at", compact_at)
         ix.set_option("union_w", union_w)
         ix.set_option("union_defer", defer)
+        ix.set_option("union_inplace", inplace)
         ix.set_option("tight_at", tight)
         ix.set_option("cold_bound", cold)
         D, I = ix.search(xq, k)
         assert_parity(D, I, Dr, Ir)
         print(f"\n[scan-options] {kind} {dtype} compact_at={compact_at} union_w={union_w} "
-              f"union_defer={defer} tight_at={tight} cold_bound={cold}: fallbacks {ix.last_fallbacks()}/{nq}")
+              f"union_defer={defer} tight_at={tight} cold_bound={cold} union_inplace={inplace}: fallbacks {ix.last_fallbacks()}/{nq}")

@@ -89,7 +89,9 @@ struct Options {
                              // on by default, one-query call -7 % on a 100k x 384 fp32 index, r5r)
     int place = -1;          // FX_SCAN_PLACE: scan block placement (-1 automatic, 0, 1)
     int sx = 0;              // FX_SCAN_SX: corpus splits per XCD under placement 1 (0 automatic)
-    int reduce_cand = 1;     // FX_REDUCE_CAND: merge 16 splits' lists before the refine (small nq)
+    int reduce_cand = 1;     // FX_REDUCE_CAND: small nq over many splits: 1 one 16-wave workgroup refine per
+                             // query (k_refine_wg), 2 merge 16 splits' lists first (k_reduce_cand, round 3),
+                             // 0 the one-wave-per-query refine
     int f32_split = 1;       // FX_F32_SPLIT: fp32 indexes scan their split-bf16 image
     int centre = 1;          // FX_CENTER: L2 scan images are centred on a row sample's mean
     int pub = 1;             // FX_SCAN_PUB: union threshold over published per-split lists
@@ -164,7 +166,7 @@ struct Options {
             {"search_graph", &search_graph, 0, 1, nullptr, 0},
             {"scan_place", &place, -1, 1, nullptr, 0},
             {"scan_sx", &sx, 0, 1 << 16, nullptr, 0},
-            {"reduce_cand", &reduce_cand, 0, 1, nullptr, 0},
+            {"reduce_cand", &reduce_cand, 0, 2, nullptr, 0},
             {"f32_split", &f32_split, 0, 1, nullptr, 0},
             {"centre", &centre, 0, 1, nullptr, 0},
             {"scan_pub", &pub, 0, 1, nullptr, 0},
@@ -204,6 +206,30 @@ enum ImageKind {
     IMG_NONE = 0,  // the stored rows with srcC = |y|^2 (IP: no row constant)
     IMG_F32S = 1,  // fp32 index: [hi | lo] bf16 planes of fl(y - mu), srcC = |y - mu|^2
     IMG_C16 = 2,   // bf16 / fp16 L2 index: the stored rows, srcC = |y - mu|^2 (the query operand is x - mu)
+};
+
+}  // namespace
+
+namespace {
+
+// The device-side plan of one search: scan, refine and fallback parameters
+// over the index's workspace.  Sizes the workspace (a no-op when it is large
+// enough already, as it is for a graph capture right after do_search).
+struct SearchPlan {
+    int64_t nq = 0, nq_pad = 0;
+    int k = 0, q_dtype = F32, scan_dt = F32;
+    ScanParams sp{};
+    RefineParams rp{};
+    PrepParams pp{};
+    bool reduce = false;
+    size_t ncand = 0;
+    // the re-scan of the queries pass 1 left uncertified (plan_rescan)
+    ScanParams sp2{};
+    RefineParams rp2{};
+    PrepParams pp2{};
+    int* n_exact = nullptr;  // queries the re-scan left uncertified too (-> exact scan)
+    int nchunks = 0;         // re-scan chunks of <= RESCAN_MAX flagged queries each
+    int* chunk_cnt = nullptr;  // [nchunks] live queries of each chunk (k_rescan_chunks, on the device)
 };
 
 }  // namespace
@@ -248,10 +274,15 @@ struct FxIndex {
     std::vector<uint64_t> gkey;
     bool gfailed = false;
     void* ghq = nullptr;
-    float* ghD = nullptr;
-    int64_t* ghI = nullptr;
-    int* ghnf = nullptr;
-    size_t ghq_bytes = 0, ghd_n = 0;
+    char* ghout = nullptr;  // pinned mirror of hout for the graph's one D2H copy
+    size_t ghq_bytes = 0, ghout_bytes = 0;
+    SearchPlan gplan;       // the captured search's plan (its fallback chain runs eagerly when needed)
+    // host-output searches: ONE packed device buffer [D | I | n_drop | n_flag |
+    // flag list] (host_out_layout) and its pinned mirror, so the common case
+    // returns through one D2H copy
+    DevBuf hout;
+    char* hpin = nullptr;
+    size_t hpin_bytes = 0;
     int64_t last_fallbacks = 0;
     // uncertified count of the last search, copied stream-ordered into pinned
     // memory; read (after a stream sync) only when asked for (fb_pending)
@@ -351,7 +382,9 @@ void plan_scan(const FxIndex* h, int64_t nq, int k, ScanParams& p) {
     p.tight_at = p.share && h->opt.tight_at > KP ? h->opt.tight_at : 0;
     p.cold_bound = 0;  // below, once the split count is known
     const int ntl = p.n_qtiles, nct = p.n_ctiles;
-    constexpr int min_tiles = 4;
+    // >= 3 tiles per split: a 100k-row index (782 tiles) then fills all 256
+    // CUs with one query tile (256 splits; 192 at 4 tiles)
+    constexpr int min_tiles = 3;
     // placement (map_tile): corpus-partitioned by default (config (d): 257 vs
     // 742 GB fetched past L2 per launch, ~2 % faster); scan_place = 0 forces
     // the query-tile groups of round 1.  Also for fewer than 8 query tiles:
@@ -398,11 +431,11 @@ void plan_scan(const FxIndex* h, int64_t nq, int k, ScanParams& p) {
 // k > KP: approx candidates the refine re-ranks exactly (k_refine_big)
 int big_k1(int k) { return k > KP ? std::max(2 * k, 64) : 0; }
 
-// small batches over many splits: merge the candidate lists 16 splits at a
-// time before the refine (k_reduce_cand)
-bool use_reduce(const FxIndex* h, int k, int64_t nq, int splits) {
-    return k <= KP && nq <= 256 && splits >= 64 && h->opt.reduce_cand != 0;
-}
+// small batches over many splits (k <= KP, nq <= 256, >= 64 splits): the
+// candidate walk is shared by the waves of one workgroup per query
+// (reduce_cand 1, k_refine_wg) or by a separate merge of 16 splits' lists at a
+// time before the refine (reduce_cand 2, k_reduce_cand)
+bool small_many(int k, int64_t nq, int splits) { return k <= KP && nq <= 256 && splits >= 64; }
 
 hipError_t ensure_pinned_count(FxIndex* h) {
     if (h->pin_nf) return hipSuccess;
@@ -470,25 +503,6 @@ hipError_t update_scan_image(FxIndex* h) {
     return e;
 }
 
-// The device-side plan of one search: scan, refine and fallback parameters
-// over the index's workspace.  Sizes the workspace (a no-op when it is large
-// enough already, as it is for a graph capture right after do_search).
-struct SearchPlan {
-    int64_t nq = 0, nq_pad = 0;
-    int k = 0, q_dtype = F32, scan_dt = F32;
-    ScanParams sp{};
-    RefineParams rp{};
-    PrepParams pp{};
-    bool reduce = false;
-    size_t ncand = 0;
-    // the re-scan of the queries pass 1 left uncertified (plan_rescan)
-    ScanParams sp2{};
-    RefineParams rp2{};
-    PrepParams pp2{};
-    int* n_exact = nullptr;  // queries the re-scan left uncertified too (-> exact scan)
-    int nchunks = 0;         // re-scan chunks of <= RESCAN_MAX flagged queries each
-    int* chunk_cnt = nullptr;  // [nchunks] live queries of each chunk (k_rescan_chunks, on the device)
-};
 
 // The re-scan of the queries pass 1 could not certify (rows flag_list[0 ..
 // n_flag) of the batch, gathered on the device): the same MFMA scan over
@@ -568,11 +582,14 @@ hipError_t plan_rescan(FxIndex* h, SearchPlan& P) {
     rp.n_flag = P.n_exact;
     rp.flag_list = P.n_exact + 1;
     rp.force_fb = h->opt.force_fallback == 2;
+    rp.wg = 0;
     return hipSuccess;
 }
 
+// words (non-null: a host-output search): [n_drop | n_flag | flag list[nq]]
+// inside the packed output buffer; otherwise the index's own counter words
 hipError_t plan_search(FxIndex* h, int64_t nq, const void* qdev, int q_dtype, int k, float* Dd, int64_t* Id,
-                       SearchPlan& P) {
+                       int* words, SearchPlan& P) {
     hipError_t e;
     P.nq = nq;
     P.k = k;
@@ -658,9 +675,9 @@ hipError_t plan_search(FxIndex* h, int64_t nq, const void* qdev, int q_dtype, in
     rp.id_offset = h->id_offset;
     rp.D = Dd;
     rp.I = Id;
-    rp.n_flag = (int*)h->flag.p;
+    rp.n_flag = words ? words + 1 : (int*)h->flag.p;
     rp.flag_list = rp.n_flag + 1;
-    rp.n_drop = h->dev_drop;
+    rp.n_drop = words ? words : h->dev_drop;
     // small batches: one wave per query walks splits * KP candidates (256 splits
     // at nq = 1); issue 4 chunks of loads at a time (nq = 1: 0.84 -> ~0.3 ms)
     rp.prefetch = nq <= 256 ? 4 : 1;
@@ -669,7 +686,8 @@ hipError_t plan_search(FxIndex* h, int64_t nq, const void* qdev, int q_dtype, in
     rp.gtau = sp.share ? sp.gtau : nullptr;
     rp.nq_dev = nullptr;
     rp.out_idx = nullptr;
-    P.reduce = use_reduce(h, k, nq, sp.splits);
+    P.reduce = small_many(k, nq, sp.splits) && h->opt.reduce_cand == 2;
+    rp.wg = small_many(k, nq, sp.splits) && h->opt.reduce_cand == 1 ? 1 : 0;
     if (P.reduce) {
         const size_t nred = (size_t)sp.n_qtiles * ((sp.splits + 15) / 16) * TILE_Q * KP;
         if ((e = h->cand2_d.ensure(nred * 4)) != hipSuccess) return e;
@@ -681,23 +699,22 @@ hipError_t plan_search(FxIndex* h, int64_t nq, const void* qdev, int q_dtype, in
     return plan_rescan(h, P);
 }
 
-// Enqueue the planned search on s: query preparation, scan, candidate
-// reduction, refine + certification, device-gated exact fallback.  No host
-// synchronisation: the same sequence is what a search graph captures.
-hipError_t enqueue_search(FxIndex* h, SearchPlan& P, hipStream_t s, bool timed, hipEvent_t* ev) {
+// Enqueue the planned search on s up to its certification: query preparation
+// (which also resets the shared thresholds, the published lists and the
+// search's counters: one kernel instead of memsets), scan, refine +
+// certification (small batches over many splits: one workgroup per query,
+// or the separate candidate reduction when asked for).  No host sync: the
+// same sequence is what a search graph captures.
+hipError_t enqueue_main(FxIndex* h, SearchPlan& P, hipStream_t s, bool timed, hipEvent_t* ev) {
     hipError_t e;
-    // the query preparation also resets the shared thresholds (ord(+inf)) and
-    // the dropped / flagged / exact counters (one kernel instead of memsets)
     PrepParams pp1 = P.pp;
     pp1.gtau = P.sp.gtau;
     pp1.zero[0] = P.rp.n_drop;
     pp1.zero[1] = P.rp.n_flag;
     pp1.zero[2] = P.n_exact;
+    pp1.pub = P.sp.pub;  // only live queries publish: nq rows of [splits][KP]
+    pp1.npub = P.sp.pub ? P.nq * P.sp.splits * KP : 0;
     if ((e = launch_prep_queries(pp1, s)) != hipSuccess) return e;
-    if (P.sp.pub) {
-        const size_t npub = (size_t)P.sp.n_qtiles * TILE_Q * P.sp.splits * KP;
-        if ((e = hipMemsetD32Async((hipDeviceptr_t)P.sp.pub, 0x7f800000u, npub, s)) != hipSuccess) return e;  // +inf
-    }
     if (timed && (e = hipEventRecord(ev[0], s)) != hipSuccess) return e;
     if ((e = launch_scan(P.scan_dt, h->metric, P.sp, s)) != hipSuccess) return e;
     if (timed && (e = hipEventRecord(ev[1], s)) != hipSuccess) return e;
@@ -713,12 +730,18 @@ hipError_t enqueue_search(FxIndex* h, SearchPlan& P, hipStream_t s, bool timed, 
     }
     if ((e = launch_refine(h->dtype, h->metric, rp, s)) != hipSuccess) return e;
     if (timed && (e = hipEventRecord(ev[2], s)) != hipSuccess) return e;
-    // Certification result: uncertified queries (rare: only when the
-    // candidate margin is inside the scan's rounding bound) are re-scanned
-    // with a wide candidate set (plan_rescan), and what that still cannot
-    // certify is re-ranked by the exact scan.  Decided on the device: these
-    // kernels are always enqueued and exit at once when nothing was flagged,
-    // so no host round trip sits inside the search.
+    return hipSuccess;
+}
+
+// The chain for the queries the refine could not certify (rare: only when the
+// candidate margin is inside the scan's rounding bound): a re-scan with a
+// wide candidate set (plan_rescan), then the exact scan for what that still
+// cannot certify.  Device-gated: every kernel reads the flagged count and
+// exits at once when it is 0.  A device-resident search enqueues it always
+// (no host round trip inside the search); a host-output search enqueues it
+// only when its packed result says some query was flagged (finish_host_out).
+hipError_t enqueue_fallback(FxIndex* h, SearchPlan& P, hipStream_t s) {
+    hipError_t e;
 #ifdef FX_ABLATION
     if ((P.sp.dbg & ~32) != 0) return hipSuccess;  // ablated scans: results invalid, no fallback chain
 #endif
@@ -729,6 +752,8 @@ hipError_t enqueue_search(FxIndex* h, SearchPlan& P, hipStream_t s, bool timed, 
         pp.qidx = list;
         pp.nq_dev = P.chunk_cnt + c;
         pp.zero[0] = pp.zero[1] = pp.zero[2] = nullptr;
+        pp.pub = nullptr;
+        pp.npub = 0;
         ScanParams sp = P.sp2;
         pp.gtau = sp.gtau;  // reset by the chunk's query preparation
         sp.nq_dev = P.chunk_cnt + c;
@@ -742,6 +767,34 @@ hipError_t enqueue_search(FxIndex* h, SearchPlan& P, hipStream_t s, bool timed, 
     return launch_exact_fallback(h->dtype, h->metric, h->codes, h->row_bytes, h->kdim, h->ntotal, P.rp.qf32,
                                  P.n_exact, P.k, h->id_offset, (float*)h->fbc_d.p, (int*)h->fbc_i.p, P.rp.D, P.rp.I,
                                  s);
+}
+
+// Host-output searches (the reference's call form) return through ONE packed
+// device buffer, copied back with one D2H:
+//   [D: nq k f32 | I: nq k i64 | n_drop | n_flag | flag list: nq i32]
+// (the copy covers D .. n_flag; the flag list stays on the device for the
+// fallback chain)
+struct HostOut {
+    size_t offI = 0, offW = 0, copy_bytes = 0, bytes = 0;
+};
+HostOut host_out_layout(int64_t nq, int k) {
+    HostOut L;
+    L.offI = (size_t)round_up(nq * k * 4, 8);
+    L.offW = L.offI + (size_t)nq * k * 8;
+    L.copy_bytes = L.offW + 8;
+    L.bytes = L.offW + (size_t)(2 + nq) * 4;
+    return L;
+}
+
+hipError_t ensure_pinned(char*& p, size_t& have, size_t want) {
+    if (want <= have) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    have = 0;
+    const size_t grow = std::max(want, have + have / 2);
+    hipError_t e = hipHostMalloc((void**)&p, grow, hipHostMallocDefault);
+    if (e == hipSuccess) have = grow;
+    return e;
 }
 
 #ifdef FX_DIAG
@@ -766,6 +819,30 @@ int integrity_error(const FxIndex* h) {
                    (long long)h->last_dropped, (long long)h->ntotal);
 }
 
+// A host-output search after its packed copy landed in `pin` (the stream is
+// synchronised): when the refine flagged queries, run their fallback chain
+// now and copy the results again (rare); then hand D / I to the caller.
+int finish_host_out(FxIndex* h, SearchPlan& P, const HostOut& L, char* pin, float* D, int64_t* I) {
+    hipStream_t s = h->stream();
+    const int nflag = ((const int*)(pin + L.offW))[1];
+    h->last_exact = 0;
+    if (nflag > 0) {
+        HIP_TRY(ensure_pinned_count(h));
+        HIP_TRY(enqueue_fallback(h, P, s));
+        HIP_TRY(hipMemcpyAsync(pin, P.rp.D, L.copy_bytes, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(h->pin_nf + 1, P.n_exact, 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        h->last_exact = h->pin_nf[1];
+    }
+    const int* w = (const int*)(pin + L.offW);
+    memcpy(D, pin, (size_t)P.nq * P.k * 4);
+    memcpy(I, pin + L.offI, (size_t)P.nq * P.k * 8);
+    h->last_fallbacks = nflag;
+    h->last_dropped = w[0];
+    h->fb_pending = false;
+    return h->last_dropped > 0 ? integrity_error(h) : FX_OK;
+}
+
 int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int k, float* D, int64_t* I,
               int out_mem) {
     hipStream_t s = h->stream();
@@ -777,17 +854,23 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
         HIP_TRY(hipMemcpyAsync(h->qin.p, q, (size_t)nq * h->d * qes, hipMemcpyHostToDevice, s));
         qdev = h->qin.p;
     }
+    // host results: the packed output buffer (host_out_layout)
+    const bool host_out = out_mem == FX_MEM_HOST;
+    HostOut L;
     float* Dd = D;
     int64_t* Id = I;
-    if (out_mem == FX_MEM_HOST) {
-        HIP_TRY(h->dws.ensure((size_t)nq * k * 4));
-        HIP_TRY(h->iws.ensure((size_t)nq * k * 8));
-        Dd = (float*)h->dws.p;
-        Id = (int64_t*)h->iws.p;
+    int* words = nullptr;
+    if (host_out) {
+        L = host_out_layout(nq, k);
+        HIP_TRY(h->hout.ensure(L.bytes));
+        HIP_TRY(ensure_pinned(h->hpin, h->hpin_bytes, L.copy_bytes));
+        Dd = (float*)h->hout.p;
+        Id = (int64_t*)((char*)h->hout.p + L.offI);
+        words = (int*)((char*)h->hout.p + L.offW);
     }
     HIP_TRY(update_scan_image(h));
     SearchPlan P;
-    HIP_TRY(plan_search(h, nq, qdev, q_dtype, k, Dd, Id, P));
+    HIP_TRY(plan_search(h, nq, qdev, q_dtype, k, Dd, Id, words, P));
 #ifdef FX_DIAG
     // diagnostics (Options): per-block placement/timing, phase stamps, the
     // scan's key matrix, raw candidate lists -> binary files
@@ -812,16 +895,22 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     if (h->profile)
         for (auto& x : ev) HIP_TRY(hipEventCreate(&x));
-    HIP_TRY(enqueue_search(h, P, s, h->profile, ev));
+    HIP_TRY(enqueue_main(h, P, s, h->profile, ev));
     if (h->profile) {
         h->ev_scan.emplace_back(ev[0], ev[1]);
         h->ev_merge.emplace_back(ev[1], ev[2]);
     }
-    HIP_TRY(ensure_pinned_count(h));
-    HIP_TRY(hipMemcpyAsync(h->pin_nf, P.rp.n_flag, 4, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(h->pin_nf + 1, P.n_exact, 4, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(h->pin_nf + 2, P.rp.n_drop, 4, hipMemcpyDeviceToHost, s));
-    h->fb_pending = true;
+    if (!host_out) {
+        // device results: the uncertified queries' chain is enqueued always and
+        // decided on the device; the counts follow stream-ordered into pinned
+        // memory, read only when asked for (read_counts)
+        HIP_TRY(enqueue_fallback(h, P, s));
+        HIP_TRY(ensure_pinned_count(h));
+        HIP_TRY(hipMemcpyAsync(h->pin_nf, P.rp.n_flag, 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(h->pin_nf + 1, P.n_exact, 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(h->pin_nf + 2, P.rp.n_drop, 4, hipMemcpyDeviceToHost, s));
+        h->fb_pending = true;
+    }
 #ifdef FX_DIAG
     if (!h->opt.cand.empty()) {
         HIP_TRY(hipStreamSynchronize(s));
@@ -845,17 +934,11 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
         HIP_TRY(dump_device<unsigned long long>(h->opt.trace, P.sp.trace, grid * 4));
     }
 #endif
-    if (out_mem == FX_MEM_HOST) {
-        HIP_TRY(hipMemcpyAsync(D, Dd, (size_t)nq * k * 4, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipMemcpyAsync(I, Id, (size_t)nq * k * 8, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        h->last_fallbacks = h->pin_nf[0];
-        h->last_exact = h->pin_nf[1];
-        h->last_dropped = h->pin_nf[2];
-        h->fb_pending = false;
-        if (h->last_dropped > 0) return integrity_error(h);
-    }
-    return FX_OK;
+    if (!host_out) return FX_OK;
+    // host results: ONE packed D2H copy [D | I | n_drop | n_flag]
+    HIP_TRY(hipMemcpyAsync(h->hpin, h->hout.p, L.copy_bytes, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return finish_host_out(h, P, L, h->hpin, D, I);
 }
 
 // k > FX_BIG_K: exact keys of every (query, row) pair and a radix sort per
@@ -932,7 +1015,7 @@ std::vector<uint64_t> graph_key(const FxIndex* h, int64_t nq, int q_dtype, int k
             (uint64_t)(uintptr_t)h->qeps.p, (uint64_t)(uintptr_t)h->qrho.p, (uint64_t)(uintptr_t)h->gtau.p,
             (uint64_t)(uintptr_t)h->pub.p, (uint64_t)(uintptr_t)h->cand_d.p, (uint64_t)(uintptr_t)h->cand_i.p,
             (uint64_t)(uintptr_t)h->cand2_d.p, (uint64_t)(uintptr_t)h->cand2_i.p,
-            (uint64_t)(uintptr_t)h->dws.p, (uint64_t)(uintptr_t)h->iws.p,
+            (uint64_t)(uintptr_t)h->hout.p,
             (uint64_t)(uintptr_t)h->flag.p, (uint64_t)(uintptr_t)h->fbc_d.p, (uint64_t)(uintptr_t)h->fbc_i.p,
             (uint64_t)(uintptr_t)h->rq_f32.p, (uint64_t)(uintptr_t)h->rq_op.p, (uint64_t)(uintptr_t)h->rq_eps.p,
             (uint64_t)(uintptr_t)h->rq_rho.p, (uint64_t)(uintptr_t)h->rq_shift.p, (uint64_t)(uintptr_t)h->rq_gtau.p,
@@ -947,13 +1030,15 @@ void graph_release(FxIndex* h) {
 }
 
 // Record the stream-ordered search of do_search (host queries, host results,
-// no diagnostics) into h->gexec.  Runs right after a do_search of the same
-// shape, so every workspace is sized and every kernel attribute set; the
-// enqueued sequence is do_search's own (enqueue_search).
+// no diagnostics) into h->gexec: the query's H2D copy, enqueue_main (prep,
+// scan, refine: no fallback chain) and the packed result's one D2H copy.
+// Runs right after a do_search of the same shape, so every workspace is
+// sized and every kernel attribute set.
 hipError_t graph_build(FxIndex* h, int64_t nq, int q_dtype, int k) {
     graph_release(h);
     hipStream_t s = h->stream();
-    const size_t qb = (size_t)nq * h->d * dtype_size(q_dtype), nd = (size_t)nq * k;
+    const size_t qb = (size_t)nq * h->d * dtype_size(q_dtype);
+    const HostOut L = host_out_layout(nq, k);
     hipError_t e = hipSuccess;
     if (qb > h->ghq_bytes) {
         if (h->ghq) (void)hipHostFree(h->ghq);
@@ -962,31 +1047,21 @@ hipError_t graph_build(FxIndex* h, int64_t nq, int q_dtype, int k) {
         if ((e = hipHostMalloc(&h->ghq, qb, hipHostMallocDefault)) != hipSuccess) return e;
         h->ghq_bytes = qb;
     }
-    if (nd > h->ghd_n) {
-        if (h->ghD) (void)hipHostFree(h->ghD);
-        if (h->ghI) (void)hipHostFree(h->ghI);
-        h->ghD = nullptr;
-        h->ghI = nullptr;
-        h->ghd_n = 0;
-        if ((e = hipHostMalloc((void**)&h->ghD, nd * 4, hipHostMallocDefault)) != hipSuccess) return e;
-        if ((e = hipHostMalloc((void**)&h->ghI, nd * 8, hipHostMallocDefault)) != hipSuccess) return e;
-        h->ghd_n = nd;
-    }
-    if (!h->ghnf && (e = hipHostMalloc((void**)&h->ghnf, 12, hipHostMallocDefault)) != hipSuccess) return e;
-    SearchPlan P;
-    if ((e = plan_search(h, nq, h->qin.p, q_dtype, k, (float*)h->dws.p, (int64_t*)h->iws.p, P)) != hipSuccess)
+    if ((e = ensure_pinned(h->ghout, h->ghout_bytes, L.copy_bytes)) != hipSuccess) return e;
+    if ((e = h->hout.ensure(L.bytes)) != hipSuccess) return e;  // (sized by the do_search before)
+    char* hb = (char*)h->hout.p;
+    SearchPlan& P = h->gplan;
+    P = SearchPlan{};
+    if ((e = plan_search(h, nq, h->qin.p, q_dtype, k, (float*)hb, (int64_t*)(hb + L.offI), (int*)(hb + L.offW),
+                         P)) != hipSuccess)
         return e;
     P.sp.dbg = 0;
 
     if ((e = hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal)) != hipSuccess) return e;
     g_graph_capture = true;
     hipError_t ce = hipMemcpyAsync(h->qin.p, h->ghq, qb, hipMemcpyHostToDevice, s);
-    if (ce == hipSuccess) ce = enqueue_search(h, P, s, false, nullptr);
-    if (ce == hipSuccess) ce = hipMemcpyAsync(h->ghD, P.rp.D, nd * 4, hipMemcpyDeviceToHost, s);
-    if (ce == hipSuccess) ce = hipMemcpyAsync(h->ghI, P.rp.I, nd * 8, hipMemcpyDeviceToHost, s);
-    if (ce == hipSuccess) ce = hipMemcpyAsync(h->ghnf, P.rp.n_flag, 4, hipMemcpyDeviceToHost, s);
-    if (ce == hipSuccess) ce = hipMemcpyAsync(h->ghnf + 1, P.n_exact, 4, hipMemcpyDeviceToHost, s);
-    if (ce == hipSuccess) ce = hipMemcpyAsync(h->ghnf + 2, P.rp.n_drop, 4, hipMemcpyDeviceToHost, s);
+    if (ce == hipSuccess) ce = enqueue_main(h, P, s, false, nullptr);
+    if (ce == hipSuccess) ce = hipMemcpyAsync(h->ghout, hb, L.copy_bytes, hipMemcpyDeviceToHost, s);
     g_graph_capture = false;
     hipGraph_t graph = nullptr;
     e = hipStreamEndCapture(s, &graph);  // always end the capture: the stream must leave capture mode
@@ -1002,9 +1077,10 @@ hipError_t graph_build(FxIndex* h, int64_t nq, int q_dtype, int k) {
     return hipSuccess;
 }
 
-// Small host batches under search_graph: replay the captured search (the
-// exact fallback included: it is device-gated); on a shape / buffer / option
-// change run do_search and re-capture.
+// Small host batches under search_graph: replay the captured search; its
+// fallback chain runs eagerly only when the packed result flags a query
+// (finish_host_out).  On a shape / buffer / option change run do_search and
+// re-capture.
 int graph_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int k, float* D, int64_t* I) {
     HIP_TRY(update_scan_image(h));
     if (h->gexec && graph_key(h, nq, q_dtype, k) == h->gkey) {
@@ -1012,13 +1088,7 @@ int graph_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int k, floa
         memcpy(h->ghq, q, (size_t)nq * h->d * dtype_size(q_dtype));
         HIP_TRY(hipGraphLaunch(h->gexec, s));
         HIP_TRY(hipStreamSynchronize(s));
-        memcpy(D, h->ghD, (size_t)nq * k * 4);
-        memcpy(I, h->ghI, (size_t)nq * k * 8);
-        h->last_fallbacks = h->ghnf[0];
-        h->last_exact = h->ghnf[1];
-        h->last_dropped = h->ghnf[2];
-        h->fb_pending = false;
-        return h->last_dropped > 0 ? integrity_error(h) : FX_OK;
+        return finish_host_out(h, h->gplan, host_out_layout(nq, k), h->ghout, D, I);
     }
     const int rc = do_search(h, nq, q, q_dtype, FX_MEM_HOST, k, D, I, FX_MEM_HOST);
     if (rc == FX_OK && !h->gfailed) {
@@ -1102,13 +1172,12 @@ void fx_index_free(FxIndex* h) {
                           &h->fbc_d, &h->fbc_i, &h->stage, &h->gtau, &h->trace, &h->dbgbuf, &h->split, &h->cnorms,
                           &h->centre, &h->mu_part, &h->qshift, &h->qrho, &h->stamps, &h->pub, &h->cand2_d,
                           &h->cand2_i, &h->rq_f32, &h->rq_op, &h->rq_eps, &h->rq_rho, &h->rq_shift, &h->rq_gtau,
-                          &h->rq_cand_d, &h->rq_cand_i, &h->rq_flag, &h->hk_ws})
+                          &h->rq_cand_d, &h->rq_cand_i, &h->rq_flag, &h->hk_ws, &h->hout})
             b->release();
         graph_release(h);
         if (h->ghq) (void)hipHostFree(h->ghq);
-        if (h->ghD) (void)hipHostFree(h->ghD);
-        if (h->ghI) (void)hipHostFree(h->ghI);
-        if (h->ghnf) (void)hipHostFree(h->ghnf);
+        if (h->ghout) (void)hipHostFree(h->ghout);
+        if (h->hpin) (void)hipHostFree(h->hpin);
         if (h->pin_nf) (void)hipHostFree(h->pin_nf);
         for (auto& pr : h->ev_scan) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
         for (auto& pr : h->ev_merge) (void)hipEventDestroy(pr.second);

@@ -116,7 +116,11 @@ struct RefineParams {
     int64_t ntotal;        // rows of the index: a candidate row id outside [0, ntotal) is never gathered
     int* n_drop;           // ... and counted here (ids other than -1 outside [0, ntotal): a corrupted
                            // candidate list), read back by fx_index_last_dropped_candidates
+    int wg;                // 1: small batches over many splits (k <= KP): one 16-wave workgroup per query
+                           // (k_refine_wg: the waves share the walk over splits * KP candidates); 0: k_refine
 };
+// waves of k_refine_wg's workgroup (one query per workgroup)
+constexpr int REFINE_WG_WAVES = 16;
 
 // exact fallback (k_fb_scan / k_fb_merge): corpus splits per flagged query,
 // decided on the device from the flagged count nf; items nf * fbs <=
@@ -168,6 +172,8 @@ struct PrepParams {
     // the search's resets, folded into this first kernel instead of memsets:
     unsigned* gtau;         // non-null: [nq_pad] the scan's shared thresholds, set to ord(+inf)
     int* zero[3];           // non-null entries: counters set to 0 (dropped ids, flagged, exact)
+    float* pub;             // non-null: the scan's published lists, npub floats set to +inf
+    int64_t npub;
 };
 hipError_t launch_prep_queries(const PrepParams& p, hipStream_t s);
 hipError_t launch_scan(int st_dt, int metric, const ScanParams& p, hipStream_t s);

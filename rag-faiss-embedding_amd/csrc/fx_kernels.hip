@@ -458,6 +458,10 @@ __global__ __launch_bounds__(256) void k_split_rows(const float* __restrict__ co
 __global__ __launch_bounds__(256) void k_prep_queries(PrepParams p, double gamma) {
     const int lane = threadIdx.x & 63;
     const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (p.pub) {  // the published lists of the scan's union bound -> +inf (grid-stride)
+        const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < p.npub; i += stride) p.pub[i] = FX_INF;
+    }
     if (r >= p.nq_pad) return;
     if (lane == 0) {
         if (p.gtau) p.gtau[r] = 0xff800000u;  // f2ord(+inf)
@@ -969,11 +973,166 @@ __global__ __launch_bounds__(256) void k_refine(RefineParams p) {
     // Rows the selection dropped all have approx key >= td (DESIGN.md
     // "certification"); they cannot outrank the k-th result when
     // key_k < td (+|x|^2 for L2) - eps.
-    if (nvalid >= KP) {
+    // Fewer than KP candidates in all: nothing was dropped unless some split
+    // pruned with a threshold, and every pruning threshold of the scan is
+    // published to the shared one (compactions, the cold-start bound), so a
+    // finite gtau means "certify" 
+    const unsigned gq = p.gtau ? p.gtau[q] : 0xff800000u;
+    if (nvalid >= KP || gq < 0xff800000u) {
         const float kth = __shfl(key, p.k - 1, 64);
         // a split may also have pruned with the shared threshold (a bound on
         // a rank below KP, compact_wave): dropped rows lie above min(td, it)
-        const float tb = p.gtau ? fminf(td, ord2f(p.gtau[q])) : td;
+        const float tb = p.gtau ? fminf(td, ord2f(gq)) : td;
+        if (!certified(kth, tb, p, q) && lane == 0 && !p.force_fb) {
+            const int pos = atomicAdd(p.n_flag, 1);
+            p.flag_list[pos] = (int)q;
+        }
+    }
+    if (p.force_fb && lane == 0) {
+        const int pos = atomicAdd(p.n_flag, 1);
+        p.flag_list[pos] = (int)q;
+    }
+}
+
+// refine_take for a chunk that is two ascending runs of KP = 32 (lanes 0-31,
+// 32-63): two consecutive splits' lists as the scan flushed them (sorted by
+// (key, row)).  Reversing the upper run makes the chunk bitonic, so a 6-step
+// merge replaces the 21-step sort; a chunk that is not two sorted runs (a
+// corrupted id masked to INT_MAX, -0 against +0 keys) takes the full sort.
+__device__ __forceinline__ void refine_take2(float d, int i, float& bd, int& bi, float& td, int& ti, int& nvalid,
+                                             int lane) {
+    nvalid += __popcll(__ballot(i != INT_MAX));
+    const bool pass = i != INT_MAX && key_lt(d, i, td, ti);
+    if (!__any(pass)) return;
+    if (!pass) { d = FX_INF; i = INT_MAX; }  // (a suffix of each sorted run)
+    const float pd = __shfl(d, lane - 1, 64);
+    const int pi = __shfl(i, lane - 1, 64);
+    if (__any((lane & 31) != 0 && key_lt(d, i, pd, pi))) {
+        sort64(d, i, lane);
+    } else {
+        const int src = lane < 32 ? lane : 95 - lane;
+        d = __shfl(d, src, 64);
+        i = __shfl(i, src, 64);
+        merge64(d, i, lane);
+    }
+    merge_into(bd, bi, d, i, lane);
+    td = __shfl(bd, KP - 1, 64);
+    ti = __shfl(bi, KP - 1, 64);
+}
+
+// Small batches over many corpus splits (the reference's one-query call: 192
+// splits on a 100k-row index, 1,024 on 10M rows): one workgroup of
+// REFINE_WG_WAVES waves per query instead of k_reduce_cand + k_refine (one
+// launch less on the latency-bound path, and the candidate walk in
+// parallel).  Each wave walks every NW-th chunk of the query's splits * KP
+// candidates into its own top KP (refine_take2: chunks are pairs of sorted
+// split lists); the NW lists are merged pairwise in LDS (log2 NW bitonic
+// merges) into the query's top KP -- the union of the waves' top KP holds
+// the global top KP under the (key, id) order, so the selection, its KP-th
+// key td and the candidate count are k_refine's; the exact re-rank of the KP
+// rows is spread over the waves, and wave 0 orders, writes and certifies
+// exactly as k_refine does.
+template <int DT, int METRIC, int NW>
+__global__ __launch_bounds__(64 * NW) void k_refine_wg(RefineParams p) {
+    static_assert((NW & (NW - 1)) == 0 && NW >= 2, "pairwise merge tree");
+    constexpr int PF = 4;
+    __shared__ float s_d[NW * KP];
+    __shared__ int s_i[NW * KP];
+    __shared__ int s_nv[NW];
+    __shared__ double s_ex[KP];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t q = blockIdx.x;
+    if (q >= p.nq) return;  // (block-uniform)
+    const int qtile = (int)(q / TILE_Q), qq = (int)(q % TILE_Q);
+    const int ncand = p.splits * KP;
+
+    // ---- phase 1: this wave's KP best approx keys over its chunks
+    float bd = FX_INF, td = FX_INF;
+    int bi = INT_MAX, ti = INT_MAX;
+    int nvalid = 0, bad = 0;
+    for (int base = w * 64 * PF; base < ncand; base += NW * 64 * PF) {
+        float dv[PF];
+        int iv[PF];
+#pragma unroll
+        for (int u = 0; u < PF; ++u) {
+            const int c = base + u * 64 + lane;
+            dv[u] = FX_INF;
+            iv[u] = INT_MAX;
+            if (c < ncand) {
+                const int s = c / KP, j = c - s * KP;
+                const int64_t off = (((int64_t)qtile * p.splits + s) * TILE_Q + qq) * KP + j;
+                const float dd = p.cand_d[off];
+                const int ii = p.cand_i[off];
+                if (ii >= 0 && ii < p.ntotal) { dv[u] = dd; iv[u] = ii; }
+                else bad += cand_id_corrupt(ii, p.ntotal);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < PF; ++u) refine_take2(dv[u], iv[u], bd, bi, td, ti, nvalid, lane);
+    }
+    count_dropped(bad, p.n_drop, lane);
+    if (lane < KP) {
+        s_d[w * KP + lane] = bd;
+        s_i[w * KP + lane] = bi;
+    }
+    if (lane == 0) s_nv[w] = nvalid;
+    __syncthreads();
+
+    // ---- the query's top KP: pairwise bitonic merges of the waves' ascending lists
+#pragma unroll
+    for (int st = 1; st < NW; st <<= 1) {
+        if ((w & (2 * st - 1)) == 0) {
+            const int src = lane < KP ? w * KP + lane : (w + st) * KP + (63 - lane);
+            float d = s_d[src];
+            int i = s_i[src];
+            merge64(d, i, lane);
+            if (lane < KP) {
+                s_d[w * KP + lane] = d;
+                s_i[w * KP + lane] = i;
+            }
+        }
+        __syncthreads();
+    }
+    bd = lane < KP ? s_d[lane] : FX_INF;
+    bi = lane < KP ? s_i[lane] : INT_MAX;
+    td = s_d[KP - 1];
+    nvalid = 0;
+#pragma unroll
+    for (int v = 0; v < NW; ++v) nvalid += s_nv[v];
+
+    // ---- phase 2: exact fp64 values of the KP selected rows (16 lanes / row,
+    // 4 rows per wave-step; step r on wave r % NW)
+    const float* xq = p.qf32 + q * (int64_t)p.kdim;
+    const int grp = lane >> 4, sub = lane & 15;
+    for (int r = w; r < KP / 4; r += NW) {
+        const int row = __shfl(bi, r * 4 + grp, 64);
+        double a = 0.0;
+        if (row != INT_MAX) a = exact_partial<DT, METRIC>(xq, p.codes + (int64_t)row * p.row_bytes, p.row_bytes, sub, 16);
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+        if (sub == 0) s_ex[r * 4 + grp] = a;
+    }
+    __syncthreads();
+    if (w != 0) return;
+
+    // ---- phase 3 (wave 0): order by (fp32 exact key, id), write top-k, certify
+    float key = FX_INF;
+    int id = INT_MAX;
+    if (lane < KP && bi != INT_MAX) {
+        const double ex = s_ex[lane];
+        key = METRIC == L2 ? (float)ex : -(float)ex;
+        id = bi;
+    }
+    sort64(key, id, lane);
+    if (lane < p.k) {
+        const bool valid = id != INT_MAX;
+        p.D[q * p.k + lane] = valid ? (METRIC == L2 ? key : -key) : (METRIC == L2 ? FLT_MAX : -FLT_MAX);
+        p.I[q * p.k + lane] = valid ? (int64_t)id + p.id_offset : (int64_t)-1;
+    }
+    const unsigned gq = p.gtau ? p.gtau[q] : 0xff800000u;  // (k_refine: certify when anything pruned)
+    if (nvalid >= KP || gq < 0xff800000u) {
+        const float kth = __shfl(key, p.k - 1, 64);
+        const float tb = p.gtau ? fminf(td, ord2f(gq)) : td;
         if (!certified(kth, tb, p, q) && lane == 0 && !p.force_fb) {
             const int pos = atomicAdd(p.n_flag, 1);
             p.flag_list[pos] = (int)q;
@@ -1388,6 +1547,9 @@ template <int DT, int METRIC>
 static hipError_t refine_t(const RefineParams& p, hipStream_t s) {
     if (p.k > KP || p.k1 > 0)  // (k1 > 0 with k <= KP: the re-scan's wide candidate set)
         hipLaunchKernelGGL((k_refine_big<DT, METRIC>), dim3((unsigned)p.nq), dim3(BT_THREADS), 0, s, p);
+    else if (p.wg)
+        hipLaunchKernelGGL((k_refine_wg<DT, METRIC, REFINE_WG_WAVES>), dim3((unsigned)p.nq), dim3(64 * REFINE_WG_WAVES),
+                           0, s, p);
     else if (p.prefetch > 1)
         hipLaunchKernelGGL((k_refine<DT, METRIC, 4>), dim3((unsigned)((p.nq + 3) / 4)), dim3(256), 0, s, p);
     else

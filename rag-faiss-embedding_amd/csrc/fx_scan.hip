@@ -491,16 +491,25 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
             const int trow0 = (ct0 + t) * TILE_R;
             // the index's last tile: rows past ntotal (zero rows of the padding)
             // get key +inf, so no push tests a row bound (L2 padding keys are
-            // +inf already through their +inf norms; IP keys are 0)
+            // +inf already through their +inf norms; IP keys are 0).  The group
+            // minima are re-taken over the fixed keys: the cold-start bound
+            // below counts them as rows, and an IP padding group's minimum 0
+            // would otherwise stand for a real row (real rows with
+            // negative inner product were pruned on a split that starts at the
+            // index's last tile)
             if (__builtin_expect((int64_t)trow0 + TILE_R > p.ntotal, 0)) {
                 const int lim = (int)(p.ntotal - trow0);
 #pragma unroll
                 for (int m = 0; m < M; ++m)
 #pragma unroll
-                    for (int n = 0; n < N; ++n)
+                    for (int n = 0; n < N; ++n) {
 #pragma unroll
                         for (int i = 0; i < 4; ++i)
                             if (rl0 + 16 * m + i >= lim) acc[m][n][i] = FX_INF;
+                        gmin[n][m] = min4(acc[m][n]);
+                    }
+#pragma unroll
+                for (int n = 0; n < N; ++n) mn[n] = min8_raw(gmin[n]);
             }
             if (p.cold_bound) {
                 // An empty list (nothing pushed yet in this block: a split that
@@ -533,6 +542,11 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                         b = fmaxf(b, lane_xor<32>(b, lane));
                         if (qv && lr.cnt[n] == 0) {
                             tn[n] = fminf(tn[n], b);
+                            // published like a compaction's bound: every pruning
+                            // threshold is then <= the final shared one, which
+                            // k_refine certifies against even when the query's
+                            // lists hold fewer than KP candidates in all
+                            if (lane < 16 && b < lr.tau[n]) gmin_u32(gtq + 16 * n + lane, f2ord(b));
                             lr.tau[n] = fminf(lr.tau[n], b);
                         }
                     }

@@ -353,10 +353,12 @@ __device__ __forceinline__ ListRegs compact_regs(float* lst, ListRegs r, unsigne
     for (int done = 0; rest && done < inplace_max; done += 4) {
         int qs[4];
         unsigned kv[4][4];
+        // (exactly inplace_max lists in all: a round takes at most what is left of it)
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            qs[u] = rest ? __builtin_ctzll(rest) : -1;
-            if (rest) rest &= rest - 1;
+            const bool take = rest != 0 && done + u < inplace_max;
+            qs[u] = take ? __builtin_ctzll(rest) : -1;
+            if (take) rest &= rest - 1;
         }
         // every lane loads unconditionally (absent lists read entry e of the
         // first list and are masked after the load): a load under a lane

@@ -18,6 +18,7 @@ import numpy as np
 import pytest
 
 from oracle import cpu as C
+from oracle import flat_l2 as F
 from tests.test_gpu_parity import assert_parity
 
 pytestmark = pytest.mark.gpu
@@ -65,3 +66,58 @@ def test_compaction_and_union_options_exact(fx, kind, dtype, d):
         assert_parity(D, I, Dr, Ir)
         print(f"\n[scan-options] {kind} {dtype} compact_at={compact_at} union_w={union_w} "
               f"union_defer={defer} tight_at={tight} cold_bound={cold} union_inplace={inplace}: fallbacks {ix.last_fallbacks()}/{nq}")
+
+
+# --------------------------------------------------------------------------
+# Inner product and the index's padded edge tile: IP keys of
+# the zero padding rows are 0, not +inf, so a cold list whose first record tile
+# is the index's last tile must not count padding groups as rows when it
+# bounds its threshold from the tile's group minima (cold_bound).  Queries
+# anti-correlated to every row have no positive inner product at all: every
+# real key is > 0 = a padding key, which is the case the bound got wrong.
+
+def ip_rows(n, d, nq, seed, anti):
+    rng = np.random.default_rng(seed)
+    base = np.abs(rng.standard_normal(d)) + 0.5
+    xb = (base + 0.3 * rng.standard_normal((n, d))).astype(np.float32)
+    xq = (rng.standard_normal((nq, d)) * 0.3 - (base if anti else 0.0)).astype(np.float32)
+    return xb, xq
+
+
+@pytest.mark.parametrize("n", [50, 127, 10_016, 70_001])
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+@pytest.mark.parametrize("cold", [-1, 1])
+def test_inner_product_edge_tile_cold_bound(fx, n, dtype, cold):
+    d, nq, k = 64, 96, 10
+    xb, xq = ip_rows(n, d, nq, 31, anti=True)
+    ix = fx.IndexFlatIP(d, dtype=dtype)
+    ix.add(xb)
+    ix.set_option("cold_bound", cold)
+    ref = xb if dtype == "float32" else ix.reconstruct_n(0, n)
+    assert (xq.astype(np.float64) @ ref.astype(np.float64).T < 0).all()  # no positive inner product
+    D, I = ix.search(xq, k)
+    Dr, Ir = F.knn_inner_product(xq, ref, k)
+    assert (I >= 0).all()
+    assert_parity(D, I, Dr, Ir)
+
+
+@pytest.mark.parametrize("anti", [False, True])
+def test_inner_product_options_exact(fx, anti):
+    """The option sweep above on IndexFlatIP (300k rows: many short splits)."""
+    n, d, nq, k = 300_000, 256, 300, 10
+    xb, xq = ip_rows(n, d, nq, 13, anti)
+    ix = fx.IndexFlatIP(d, dtype="bfloat16")
+    ix.add(xb)
+    ref = ix.reconstruct_n(0, n)
+    Dr, Ir = F.knn_inner_product(xq, ref, k)
+    for compact_at, union_w, defer, tight, cold, inplace in [
+            (0, 0, 1, -1, -1, -1), (0, 0, 1, 0, 1, 0), (48, 64, 1, 0, 1, 3), (64, 16, 0, 33, 1, -1),
+            (40, 32, 1, 0, 0, 5)]:
+        ix.set_option("compact_at", compact_at)
+        ix.set_option("union_w", union_w)
+        ix.set_option("union_defer", defer)
+        ix.set_option("union_inplace", inplace)
+        ix.set_option("tight_at", tight)
+        ix.set_option("cold_bound", cold)
+        D, I = ix.search(xq, k)
+        assert_parity(D, I, Dr, Ir)

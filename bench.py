@@ -335,6 +335,21 @@ def latency_nq1_f32(calls, device, n=100_000, d=384, k=10, nq=1000):
     return r
 
 
+def _lib_digest():
+    from rag_faiss_embedding_amd._provenance import file_digest
+    return file_digest(_lib_path())
+
+
+def _lib_path():
+    from rag_faiss_embedding_amd import _lib
+    return Path(_lib.LIB_PATH)
+
+
+def source_digest():
+    from rag_faiss_embedding_amd._provenance import source_digest as sd
+    return sd()
+
+
 def read_pmc_traffic(cfg_name, n_local, nq, data="synthetic"):
     """HBM bytes per scan launch from a committed rocprofv3 --pmc summary of
     this same workload (profiles/pmc_scan_<cfg>[_clustered].json), and where
@@ -353,7 +368,14 @@ def read_pmc_traffic(cfg_name, n_local, nq, data="synthetic"):
         if j.get("rows_per_gpu") != n_local or j.get("nq") != nq:
             return None, None
         src = {"file": str(p.relative_to(ROOT)), "summary": j.get("source"),
-               "note": "committed rocprofv3 --pmc pass of the same workload (not this run)"}
+               "note": "committed rocprofv3 --pmc pass of the same workload (not this run)",
+               "csrc_digest": j.get("csrc_digest"), "git_head_at_summary": j.get("git_head_at_summary")}
+        here = source_digest()
+        if j.get("csrc_digest") != here:
+            # counters of other kernels than the ones this run executes: no figure
+            src["reason"] = (f"profiled sources {j.get('csrc_digest')} != this build's {here}: "
+                             "traffic not quoted")
+            return None, src
         summ = ROOT / j["source"] if j.get("source") else None
         if summ is not None and summ.exists():
             sj = json.loads(summ.read_text())
@@ -379,7 +401,7 @@ def main():
     ap.add_argument("--nq", type=int, default=0, help="override query batch")
     ap.add_argument("--rows", type=int, default=0, help="override corpus rows (testing)")
     ap.add_argument("--recall-queries", type=int, default=0,
-                    help="oracle recall sample (0: per config, SURVEY 8d: d 256, b 1000, e 32)")
+                    help="oracle recall sample (0: per config, RECALL_QUERIES: d 1000, b 1000, e 256)")
     ap.add_argument("--cpu-rows", type=int, default=1_000_000)
     ap.add_argument("--cpu-queries", type=int, default=0, help="fixed CPU sample (0: auto-size)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="target CPU baseline sample time")
@@ -519,6 +541,8 @@ def main():
             "baseline_config": args.config, "corpus_rows": n_total, "dim": d, "nq": nq, "k": k,
             "rows_per_gpu": n_local, "parallelism": f"row-shard x{world}",
         },
+        "build": {"csrc_digest": source_digest(), "lib": _lib_path().name,
+                  "lib_digest": _lib_digest()},
         "fallback_queries_last_step": fallbacks,
         "exact_fallback_queries_last_step": exact_fb,
         "dropped_candidate_ids_last_step": dropped,

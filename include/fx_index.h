@@ -94,14 +94,16 @@ int fx_index_set_stream(FxIndex* index, void* stream);
  * values come from the FX_* environment variables, read once at index
  * creation; nothing on the search path reads the environment.  Names and
  * accepted values: "search_graph" 0/1 (default 1: replay small host searches
- * as one hipGraph), "scan_place" -1/0/1, "scan_sx" >= 0, "reduce_cand" 0/1,
+ * as one hipGraph), "scan_place" -1/0/1, "scan_sx" >= 0, "reduce_cand" 0/1/2 (small
+ * batches over many splits: 1, the default, one 16-wave workgroup refine per
+ * query; 2 a separate merge of 16 splits' lists first; 0 neither),
  * "f32_split" 0/1, "centre" 0/1, "scan_pub" 0/1, "prune_rank" 0..32,
  * "compact_at" 0 (= 48) or 33..64 (list fill that triggers a compaction), "union_w"
  * 0/16/32/64 (splits per union-bound window), "union_defer" 0/1 (default 1:
  * a compaction's union bound fetched by LDS-DMA and bounded a tile later
- * instead of waited for), "union_inplace" -1..64 (lists per compaction
- * bounded by the union in place beyond the deferred ones; -1, the default:
- * 0 with union_defer, all without), "tight_at" -1/0 (off) or 33..64 (a list that took
+ * instead of waited for), "union_inplace" -1..64 (at most this many lists
+ * per compaction bounded by the union in place beyond the deferred ones; -1,
+ * the default: 0 with union_defer, all without), "tight_at" -1/0 (off) or 33..64 (a list that took
  * entries and holds at least this many gets its threshold re-bounded between
  * compactions), "cold_bound" -1/0/1 (an empty list's first record tile bounds its
  * threshold from the per-lane group minima; -1, the default: on for corpus
@@ -132,8 +134,11 @@ int fx_index_add(FxIndex* index, int64_t n, const void* x, int x_dtype, int x_me
  * k; past ntotal I = -1, D = +-FLT_MAX as faiss pads).  Blocks until results are in host memory when out_mem is
  * FX_MEM_HOST; with FX_MEM_DEVICE (queries and results on the device) it
  * is stream-ordered: it enqueues its work and returns without waiting for
- * the device (the exact fallback for uncertified queries is decided on the
- * device).  Workspace growth (first search of a larger shape) may
+ * the device (the re-scan and exact fallback for uncertified queries are
+ * enqueued always and decided on the device).  A host-output search returns
+ * through one packed device-to-host copy [D | I | counters] and enqueues
+ * that chain only when the copy says a query was uncertified (then copies
+ * again).  Workspace growth (first search of a larger shape) may
  * synchronise through hipMalloc / hipFree; so does a k > FX_MAX_K search
  * whose sort workspace exceeds 512 MiB (it is released after the call, a
  * smaller one is kept for the next). */

@@ -45,9 +45,11 @@ def load(path: Optional[Path] = None) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.argtypes = [_f32p, ctypes.c_int64, _f32p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, _f32p, _i64p, ctypes.c_int]
         fn.restype = None
-    lib.fxo_knn_exact_synth.argtypes = [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int, _f32p, ctypes.c_int64,
-                                        ctypes.c_int, _f32p, _i64p, ctypes.c_int]
-    lib.fxo_knn_exact_synth.restype = None
+    for name in ("fxo_knn_exact_synth", "fxo_knn_exact_synth_f64"):
+        fn = getattr(lib, name)
+        fn.argtypes = [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int, _f32p, ctypes.c_int64, ctypes.c_int, _f32p,
+                       _i64p, ctypes.c_int]
+        fn.restype = None
     lib.fxo_max_threads.restype = ctypes.c_int
     if path is None:
         _lib = lib
@@ -90,12 +92,16 @@ def knn_blas(xq: np.ndarray, xb: np.ndarray, k: int, nthreads: int = 0,
 
 
 def knn_exact_synth(cseed: int, nb: int, d: int, xq: np.ndarray, k: int,
-                    nthreads: int = 0) -> Tuple[np.ndarray, np.ndarray]:
+                    nthreads: int = 0, f64: bool = False) -> Tuple[np.ndarray, np.ndarray]:
+    """Exact k-NN against synthetic corpus rows [0, nb) (streamed, never
+    materialised).  Grid-valued queries take the integer path (flat_l2.c:
+    the same exact sums); f64=True forces the fp64 restatement (its check)."""
     xq = np.ascontiguousarray(xq, dtype=np.float32)
     nq = xq.shape[0]
     D = np.empty((nq, k), dtype=np.float32)
     I = np.empty((nq, k), dtype=np.int64)
-    load().fxo_knn_exact_synth(cseed, nb, d, _fp(xq), nq, k, _fp(D), _ip(I), nthreads)
+    fn = load().fxo_knn_exact_synth_f64 if f64 else load().fxo_knn_exact_synth
+    fn(cseed, nb, d, _fp(xq), nq, k, _fp(D), _ip(I), nthreads)
     return D, I
 
 

@@ -116,7 +116,67 @@ void fxo_knn_exact(const float* xq, int64_t nq, const float* xb, int64_t nb, int
 
 /* Streaming exact k-NN against the synthetic corpus rows [0, nb) of seed
  * `cseed` (generated on the fly, never materialised): used to check GPU
- * results at full BASELINE sizes (1e7..1e8 rows) on a query subset. */
+ * results at full BASELINE sizes (1e7..1e8 rows) on a query subset.
+ *
+ * The generator's values are v = n / 64 with n = b0 + b1 - 255 an integer in
+ * [-255, 255].  When every query value is on that grid too (the synthetic
+ * queries of the tests and the bench), 4096 * sum_t (x_t - y_t)^2 is the
+ * integer |nx|^2 + |ny|^2 - 2 nx.ny (< 2^31 for d <= 8192), so the exact sum
+ * -- which the fp64 restatement below also computes exactly, every partial
+ * sum of such terms being representable -- is obtained in integer arithmetic
+ * (16-bit products, 32-bit sums: vectorised) and rounded to fp32 once, the
+ * same value bit for bit (tests/test_oracle.py checks the two paths agree).
+ * Queries off the grid take the fp64 path. */
+static int on_grid(const float* xq, int64_t n, int16_t* out) {
+    for (int64_t i = 0; i < n; ++i) {
+        const float v = xq[i] * 64.0f;
+        if (!(v == floorf(v)) || v < -255.0f || v > 255.0f) return 0;
+        out[i] = (int16_t)v;
+    }
+    return 1;
+}
+
+static inline int32_t dot_i16(const int16_t* x, const int16_t* y, int d) {
+    int32_t s = 0;
+    for (int t = 0; t < d; ++t) s += (int32_t)x[t] * (int32_t)y[t];
+    return s;
+}
+
+/* dots of 4 queries x 4 rows (d a multiple of 16 on the AVX2 path: the
+ * callers pad rows and queries with zeros to d16) */
+#if defined(__AVX2__)
+#include <immintrin.h>
+static inline int32_t hsum8(__m256i v) {
+    __m128i s = _mm_add_epi32(_mm256_castsi256_si128(v), _mm256_extracti128_si256(v, 1));
+    s = _mm_add_epi32(s, _mm_shuffle_epi32(s, 0x4E));
+    s = _mm_add_epi32(s, _mm_shuffle_epi32(s, 0xB1));
+    return _mm_cvtsi128_si32(s);
+}
+static inline void dot_i16_2x4(const int16_t* x0, const int16_t* x1, const int16_t* y0, int d16, int32_t out[2][4]) {
+    __m256i a[2][4];
+    for (int u = 0; u < 2; ++u)
+        for (int v = 0; v < 4; ++v) a[u][v] = _mm256_setzero_si256();
+    for (int t = 0; t < d16; t += 16) {
+        const __m256i q0 = _mm256_loadu_si256((const __m256i*)(x0 + t));
+        const __m256i q1 = _mm256_loadu_si256((const __m256i*)(x1 + t));
+        for (int v = 0; v < 4; ++v) {
+            const __m256i r = _mm256_loadu_si256((const __m256i*)(y0 + (size_t)v * d16 + t));
+            a[0][v] = _mm256_add_epi32(a[0][v], _mm256_madd_epi16(q0, r));
+            a[1][v] = _mm256_add_epi32(a[1][v], _mm256_madd_epi16(q1, r));
+        }
+    }
+    for (int u = 0; u < 2; ++u)
+        for (int v = 0; v < 4; ++v) out[u][v] = hsum8(a[u][v]);
+}
+#else
+static inline void dot_i16_2x4(const int16_t* x0, const int16_t* x1, const int16_t* y0, int d16, int32_t out[2][4]) {
+    for (int v = 0; v < 4; ++v) {
+        out[0][v] = dot_i16(x0, y0 + (size_t)v * d16, d16);
+        out[1][v] = dot_i16(x1, y0 + (size_t)v * d16, d16);
+    }
+}
+#endif
+
 void fxo_knn_exact_synth(uint64_t cseed, int64_t nb, int d, const float* xq, int64_t nq, int k,
                          float* D, int64_t* I, int nthreads) {
     if (nthreads > 0) omp_set_num_threads(nthreads);
@@ -126,6 +186,17 @@ void fxo_knn_exact_synth(uint64_t cseed, int64_t nb, int d, const float* xq, int
 #pragma omp single
         nt = omp_get_num_threads();
     }
+    const int d16 = (d + 15) / 16 * 16;  /* zero-padded stride of the integer rows */
+    int16_t* qraw = (int16_t*)malloc(sizeof(int16_t) * (size_t)(nq > 0 ? nq : 1) * d);
+    int16_t* qi = (int16_t*)calloc((size_t)(nq > 0 ? nq : 1) * d16, sizeof(int16_t));
+    int64_t* qn = (int64_t*)malloc(sizeof(int64_t) * (size_t)(nq > 0 ? nq : 1));
+    const int grid = d <= 8192 && on_grid(xq, nq * (int64_t)d, qraw);
+    if (grid)
+        for (int64_t q = 0; q < nq; ++q) {
+            memcpy(qi + q * d16, qraw + q * d, sizeof(int16_t) * d);
+            qn[q] = dot_i16(qi + q * d16, qi + q * d16, d16);
+        }
+    free(qraw);
     /* per-thread heaps over a row partition, merged at the end */
     float* hdall = (float*)malloc(sizeof(float) * (size_t)nt * nq * k);
     int64_t* hiall = (int64_t*)malloc(sizeof(int64_t) * (size_t)nt * nq * k);
@@ -136,15 +207,46 @@ void fxo_knn_exact_synth(uint64_t cseed, int64_t nb, int d, const float* xq, int
         int64_t* hi = hiall + (size_t)t * nq * k;
         for (int64_t q = 0; q < nq; ++q) heap_init(hd + q * k, hi + q * k, k);
         float* row = (float*)malloc(sizeof(float) * d);
+        /* grid path: blocks of RB rows (generated once) x 4 queries x 4 rows */
+        enum { RB = 64 };
+        int16_t* rowi = (int16_t*)calloc((size_t)RB * d16, sizeof(int16_t));
+        int64_t yn[RB];
         int64_t r0 = nb * t / nt, r1 = nb * (t + 1) / nt;
-        for (int64_t j = r0; j < r1; ++j) {
+        for (int64_t j0 = r0; grid && j0 < r1; j0 += RB) {
+            const int nr = (int)(r1 - j0 < RB ? r1 - j0 : RB);
+            for (int r = 0; r < RB; ++r) {  /* rows past the block's end: zero (never offered) */
+                int16_t* y = rowi + (size_t)r * d16;
+                for (int c = 0; c < d; ++c)
+                    y[c] = r < nr ? (int16_t)(synth_val(cseed, (uint64_t)(j0 + r), (uint64_t)d, (uint64_t)c) * 64.0f)
+                                  : 0;
+                yn[r] = dot_i16(y, y, d16);
+            }
+            for (int64_t q = 0; q < nq; q += 2) {
+                const int16_t* x0 = qi + (size_t)q * d16;
+                const int16_t* x1 = qi + (size_t)(q + 1 < nq ? q + 1 : q) * d16;
+                for (int r = 0; r < nr; r += 4) {
+                    int32_t dots[2][4];
+                    dot_i16_2x4(x0, x1, rowi + (size_t)r * d16, d16, dots);
+                    for (int u = 0; u < 2 && q + u < nq; ++u)
+                        for (int v = 0; v < 4 && r + v < nr; ++v) {
+                            const int64_t e = qn[q + u] + yn[r + v] - 2 * (int64_t)dots[u][v];
+                            heap_offer(hd + (q + u) * k, hi + (q + u) * k, k, (float)((double)e / 4096.0),
+                                       j0 + r + v);
+                        }
+                }
+            }
+        }
+        for (int64_t j = r0; !grid && j < r1; ++j) {
             for (int c = 0; c < d; ++c) row[c] = synth_val(cseed, (uint64_t)j, (uint64_t)d, (uint64_t)c);
-            for (int64_t q = 0; q < nq; ++q) {
-                float dist = (float)l2_exact64(xq + q * d, row, d);
-                heap_offer(hd + q * k, hi + q * k, k, dist, j);
+            {
+                for (int64_t q = 0; q < nq; ++q) {
+                    float dist = (float)l2_exact64(xq + q * d, row, d);
+                    heap_offer(hd + q * k, hi + q * k, k, dist, j);
+                }
             }
         }
         free(row);
+        free(rowi);
     }
     for (int64_t q = 0; q < nq; ++q) {
         float* od = D + q * k; int64_t* oi = I + q * k;
@@ -156,7 +258,26 @@ void fxo_knn_exact_synth(uint64_t cseed, int64_t nb, int d, const float* xq, int
             }
         heap_finish(od, oi, k);
     }
-    free(hdall); free(hiall);
+    free(hdall); free(hiall); free(qi); free(qn);
+}
+
+/* The same search on the fp64 path only (the grid shortcut off): the check of
+ * fxo_knn_exact_synth's integer path (tests/test_oracle.py). */
+void fxo_knn_exact_synth_f64(uint64_t cseed, int64_t nb, int d, const float* xq, int64_t nq, int k,
+                             float* D, int64_t* I, int nthreads) {
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int64_t q = 0; q < nq; ++q) {
+        float* hd = D + q * k; int64_t* hi = I + q * k;
+        float* row = (float*)malloc(sizeof(float) * d);
+        heap_init(hd, hi, k);
+        for (int64_t j = 0; j < nb; ++j) {
+            for (int c = 0; c < d; ++c) row[c] = synth_val(cseed, (uint64_t)j, (uint64_t)d, (uint64_t)c);
+            heap_offer(hd, hi, k, (float)l2_exact64(xq + q * d, row, d), j);
+        }
+        heap_finish(hd, hi, k);
+        free(row);
+    }
 }
 
 /* ---- FAISS BLAS-path restatement (the timed CPU baseline) ---------------- */

@@ -111,6 +111,8 @@ struct Options {
                              // at nq = 256 (short splits), +0.5-0.9 % on the long splits of (d) and the
                              // N = 8 shard (r5h, r5i, r5k)
     int graph_verbose = 0;   // FX_SEARCH_GRAPH_VERBOSE
+    int host_spin = 1;       // FX_HOST_SPIN: a host-output search waits for its results by polling the
+                             // stream (1) instead of a blocking hipStreamSynchronize (0)
 #ifdef FX_DIAG
     int force_fallback = 0;  // FX_FORCE_FALLBACK: flag every query (1: -> re-scan, 2: -> exact scan)
     int scan_dbg = 0;        // FX_SCAN_DBG: ablation switches of -DFX_ABLATION builds / key dump (32)
@@ -141,6 +143,7 @@ struct Options {
         num("FX_TIGHT_AT", tight_at);
         num("FX_COLD_BOUND", cold_bound);
         num("FX_SEARCH_GRAPH_VERBOSE", graph_verbose);
+        num("FX_HOST_SPIN", host_spin);
         (void)str;
 #ifdef FX_DIAG
         num("FX_FORCE_FALLBACK", force_fallback);
@@ -177,6 +180,7 @@ struct Options {
             {"union_inplace", &union_inplace, -1, 64, nullptr, 0},
             {"tight_at", &tight_at, -1, CAP, nullptr, 0},
             {"cold_bound", &cold_bound, -1, 1, nullptr, 0},
+            {"host_spin", &host_spin, 0, 1, nullptr, 0},
 #ifdef FX_DIAG
             {"force_fallback", &force_fallback, 0, 2, nullptr, 0},
             {"scan_dbg", &scan_dbg, 0, 1 << 20, nullptr, 0},
@@ -819,6 +823,17 @@ int integrity_error(const FxIndex* h) {
                    (long long)h->last_dropped, (long long)h->ntotal);
 }
 
+// Wait for a host-output search's results.  The one-query call is latency
+// bound: polling the stream (host_spin) returns as soon as the D2H copy is
+// done, where a blocking synchronise adds the runtime's wake-up latency.
+hipError_t wait_results(const FxIndex* h, hipStream_t s) {
+    if (!h->opt.host_spin) return hipStreamSynchronize(s);
+    for (;;) {
+        const hipError_t e = hipStreamQuery(s);
+        if (e != hipErrorNotReady) return e;
+    }
+}
+
 // A host-output search after its packed copy landed in `pin` (the stream is
 // synchronised): when the refine flagged queries, run their fallback chain
 // now and copy the results again (rare); then hand D / I to the caller.
@@ -937,7 +952,7 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
     if (!host_out) return FX_OK;
     // host results: ONE packed D2H copy [D | I | n_drop | n_flag]
     HIP_TRY(hipMemcpyAsync(h->hpin, h->hout.p, L.copy_bytes, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(wait_results(h, s));
     return finish_host_out(h, P, L, h->hpin, D, I);
 }
 
@@ -1009,6 +1024,7 @@ std::vector<uint64_t> graph_key(const FxIndex* h, int64_t nq, int q_dtype, int k
             (uint64_t)o.force_fallback, (uint64_t)o.place, (uint64_t)o.sx, (uint64_t)o.reduce_cand,
             (uint64_t)o.pub, (uint64_t)o.prune_rank, (uint64_t)o.compact_at, (uint64_t)o.union_w,
             (uint64_t)o.union_defer, (uint64_t)(int64_t)o.union_inplace, (uint64_t)(int64_t)o.tight_at, (uint64_t)o.cold_bound,
+            (uint64_t)o.reduce_cand,
             (uint64_t)(uintptr_t)h->codes, (uint64_t)(uintptr_t)h->norms, (uint64_t)(uintptr_t)h->split.p,
             (uint64_t)(uintptr_t)h->cnorms.p, (uint64_t)(uintptr_t)h->centre.p, (uint64_t)(uintptr_t)h->qshift.p,
             (uint64_t)(uintptr_t)h->qin.p, (uint64_t)(uintptr_t)h->qf32.p, (uint64_t)(uintptr_t)h->qop.p,
@@ -1087,7 +1103,7 @@ int graph_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int k, floa
         hipStream_t s = h->stream();
         memcpy(h->ghq, q, (size_t)nq * h->d * dtype_size(q_dtype));
         HIP_TRY(hipGraphLaunch(h->gexec, s));
-        HIP_TRY(hipStreamSynchronize(s));
+        HIP_TRY(wait_results(h, s));
         return finish_host_out(h, h->gplan, host_out_layout(nq, k), h->ghout, D, I);
     }
     const int rc = do_search(h, nq, q, q_dtype, FX_MEM_HOST, k, D, I, FX_MEM_HOST);

@@ -34,6 +34,7 @@ METRIC_L2 = _lib.METRIC_L2
 
 _DTYPES = {"float32": _lib.F32, "bfloat16": _lib.BF16, "float16": _lib.F16}
 _DTYPE_NAMES = {v: k for k, v in _DTYPES.items()}
+_UNBOUND = object()  # no stream bound yet by this Python object
 
 
 def _torch():
@@ -98,12 +99,11 @@ class _FlatIndex:
 
     # -- stream plumbing --------------------------------------------------------
     def _bind_stream(self, use_torch: bool) -> None:
-        if use_torch:
-            t = _torch()
-            s = t.cuda.current_stream(self.device).cuda_stream
-            self._check(self._lib.fx_index_set_stream(self._h, ctypes.c_void_p(s)))
-        else:
-            self._check(self._lib.fx_index_set_stream(self._h, None))
+        s = _torch().cuda.current_stream(self.device).cuda_stream if use_torch else None
+        if getattr(self, "_bound", _UNBOUND) == s:  # (one C call less per search on the latency-bound path)
+            return
+        self._check(self._lib.fx_index_set_stream(self._h, ctypes.c_void_p(s) if s is not None else None))
+        self._bound = s
 
     # -- add / search --------------------------------------------------------------
     def add(self, x) -> None:

@@ -120,13 +120,26 @@ class ShardedIndexFlatL2:
         faiss_store.py:61-64): the queries go to this rank's GPU once, the
         local scan, the all_gather and the merge stay on the device, and the
         merged lists come back in ONE device-to-host copy (numpy in -> numpy
-        out, a host tensor -> host tensors)."""
+        out, a host tensor -> host tensors).
+
+        A host-input search fails on EVERY rank when one rank's local search
+        failed or dropped corrupted candidate ids (one flag all_reduce before
+        the exchange), so the ranks' collectives stay in step."""
         if self.world == 1:
             return self.local.search(xq, k)
         host_in = not (isinstance(xq, torch.Tensor) and xq.is_cuda)
         if host_in and dist.get_backend(self.group) == "nccl":
             return self.search_host_on_device(xq, k)
-        D, I = self.local.search(xq, k)
+        if not host_in:  # device lists: the caller reads the integrity count (INTEGRATION.md)
+            D, I = self.local.search(xq, k)
+            return self.exchange(D, I, k)
+        D = I = None
+        why = None
+        try:
+            D, I = self.local.search(xq, k)  # host output: raises FX_E_INTEGRITY itself
+        except Exception as e:  # noqa: BLE001 -- re-raised on every rank below
+            why = f"{type(e).__name__}: {e}"
+        self._agree(why, torch.zeros(1))
         return self.exchange(D, I, k)
 
     def search_host_on_device(self, xq, k: int):
@@ -136,21 +149,38 @@ class ShardedIndexFlatL2:
         is_np = not isinstance(xq, torch.Tensor)
         xt = torch.from_numpy(np.ascontiguousarray(xq, dtype=np.float32)) if is_np else xq
         dev = self.comm_device(xt)
-        D, I = self.local.search(xt.to(dev), k)
+        D = I = None
+        why = None
+        try:
+            D, I = self.local.search(xt.to(dev), k)
+            why = self._integrity_problem()
+        except Exception as e:  # noqa: BLE001 -- re-raised on every rank below
+            why = f"{type(e).__name__}: {e}"
+        self._agree(why, xt.new_zeros(1).to(dev))
         Dm, Im = self.exchange(D, I, k)
         Dm, Im = Dm.cpu(), Im.cpu()
-        self._check_integrity()
         return (Dm.numpy(), Im.numpy()) if is_np else (Dm, Im)
 
-    def _check_integrity(self):
+    def _integrity_problem(self) -> Optional[str]:
         """A host-output search fails when the local scan's candidate lists
         held row ids outside [0, ntotal), as the single-index host search does
         (FX_E_INTEGRITY, fx_index.h): the local search here ran with device
-        outputs (stream-ordered), so its dropped count is read after the D2H
-        above has synchronised.  Device-output callers read
+        outputs (stream-ordered), so its dropped count is read (a stream sync)
+        before the exchange.  Device-output callers read
         ``local.last_dropped_candidates()`` themselves (INTEGRATION.md)."""
         dropped = getattr(self.local, "last_dropped_candidates", None)
-        if dropped is not None and dropped() > 0:
+        n = dropped() if dropped is not None else 0
+        if n > 0:
+            return f"local search dropped {n} corrupted candidate ids: its top-k may be missing rows"
+        return None
+
+    def _agree(self, why: Optional[str], like: "torch.Tensor") -> None:
+        """All ranks learn whether any rank's local search failed (one MAX
+        all_reduce of a flag on the exchange device) and then all raise
+        FxError together -- never only the failing rank, whose peers would
+        otherwise wait in the next collective."""
+        flag = torch.tensor([1.0 if why else 0.0], dtype=torch.float32, device=self.comm_device(like))
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
+        if float(flag.item()) > 0:
             from ._lib import FxError
-            raise FxError(f"local search dropped {dropped()} corrupted candidate ids: its top-k may be "
-                          "missing rows")
+            raise FxError(why if why else "the local search failed on another rank of the group")

@@ -1,7 +1,8 @@
 """GPU parity at the BASELINE.json workload shapes ("next round" 1).
 
-* (e) 100M x 384 fp16, 10k-query batch: one eighth of it (a 12.5M-row shard,
-  the per-GPU share at 8 GPUs) with the full 10k batch;
+* (e) 100M x 384 fp16, 10k-query batch: the whole 100M-row index on one GPU,
+  and one eighth of it (a 12.5M-row shard, the per-GPU share at 8 GPUs), each
+  with the full 10k batch;
 * (d) 10M x 768 bf16, 10k-query batch: the 1.25M-row shard of one GPU at 8
   GPUs, and the whole 10M corpus as 8 row shards (global id offsets) merged by
   fx_merge_shards -- the on-device step after the RCCL all_gather -- checked
@@ -92,6 +93,7 @@ def test_config_shard_full_batch(fx, torch_cuda, cfg, n, d, dtype, nsub):
     assert (Is[:, 0] == rows).all() and (Ds[:, 0] == 0).all()
 
 
+@pytest.mark.timeout(600)
 def test_config_d_eight_shards_merged(fx, torch_cuda):
     """Config (d) end to end at N=8 on one GPU: 8 contiguous row shards with
     global id offsets (sharded.shard_bounds), each searched with the full 10k
@@ -118,9 +120,34 @@ def test_config_d_eight_shards_merged(fx, torch_cuda):
     D1, I1 = ix.search(xq, k)
     np.testing.assert_array_equal(I1.cpu().numpy(), Im)
     np.testing.assert_array_equal(D1.cpu().numpy(), Dm)
-    sub = np.linspace(0, nq - 1, 128).astype(np.int64)
+    # 1,000 oracle queries over the full 10M rows (the streaming oracle's
+    # integer path: ~30-60 s on the box's host cores)
+    sub = np.linspace(0, nq - 1, 1000).astype(np.int64)
     Dr, Ir = C.knn_exact_synth(CSEED, n, d, F.synth(QSEED, 0, nq, d)[sub], k)
     assert_parity(Dm[sub], Im[sub], Dr, Ir)
+
+
+@pytest.mark.timeout(600)
+def test_config_e_full_index(fx, torch_cuda):
+    """Config (e) at its stated size on one GPU: ONE 100M x 384 fp16 index
+    (76.8 GB of codes, the north star's HBM-bound point) searched with the
+    full 10k batch.  Properties on every query (sorted lists, ids in range,
+    no fallback, self-retrieval at the index's edges); the streaming oracle
+    over all 100M rows on a 128-query subset."""
+    torch = torch_cuda
+    n, d, nq, k = 100_000_000, 384, 10_000, 10
+    ix = _synth_index(fx, torch, n, d, "float16")
+    assert ix.ntotal == n
+    xq = _queries(fx, torch, nq, d, "float16")
+    D, I = ix.search(xq, k)
+    assert ix.last_fallbacks() == 0 and ix.last_exact_fallbacks() == 0
+    D, I = _check_batch(D, I, 0, n)
+    rows = np.array([0, 1, n // 2, n - 129, n - 128, n - 2, n - 1])
+    Ds, Is = ix.search(np.concatenate([F.synth(CSEED, int(r), 1, d) for r in rows]), 2)
+    assert (Is[:, 0] == rows).all() and (Ds[:, 0] == 0).all()
+    sub = np.linspace(0, nq - 1, 128).astype(np.int64)
+    Dr, Ir = C.knn_exact_synth(CSEED, n, d, F.synth(QSEED, 0, nq, d)[sub], k)
+    assert_parity(D[sub], I[sub], Dr, Ir)
 
 
 def _tokens(torch, n, lo, hi, seed):

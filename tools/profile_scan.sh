@@ -12,6 +12,10 @@ out=gpurun_out/prof_$tag
 mkdir -p "$out"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 B="python3 bench.py --no-cpu --latency-calls 0 $*"
+# which sources / library these counters belong to (read by summarize_profile.py)
+python3 -c "import json, amd_fx; from rag_faiss_embedding_amd import _provenance as P; \
+print(json.dumps({'csrc_digest': P.source_digest(), 'lib_digest': P.file_digest('rag-faiss-embedding_amd/libfx_index.so')}))" \
+    > "$out/provenance.json"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o run -- \
     $B > "$out/trace.log" 2>&1
 pmc() {  # <subdir> <counters...>

@@ -86,6 +86,17 @@ def main():
                     pmc[c] = statistics.median(vals)
     res = {"kernels": kern, "scan_kernel": scan_name, "scan_pmc_median_per_launch": pmc,
            "rows_per_gpu": rows, "nq": nq}
+    # provenance: the profiled tree's source digest (profile_scan.sh, on the box)
+    # and the commit the summary was made at (here; the digest is the binding key)
+    prov = prof / "provenance.json"
+    if prov.exists():
+        res.update(json.loads(prov.read_text()))
+    try:
+        import subprocess
+        res["git_head_at_summary"] = subprocess.run(["git", "-C", str(ROOT), "rev-parse", "--short=12", "HEAD"],
+                                                    capture_output=True, text=True, check=True).stdout.strip()
+    except Exception:  # noqa: BLE001
+        pass
     if "FETCH_SIZE" in pmc:
         fetch = pmc["FETCH_SIZE"] * 1024 * 2          # gfx950: FETCH_SIZE = 1/2 of streamed bytes
         write = pmc.get("WRITE_SIZE", 0.0) * 1024
@@ -109,7 +120,9 @@ def main():
     if "hbm_bytes_per_launch" in res:
         (out / f"pmc_scan_{tag}.json").write_text(json.dumps(
             {"rows_per_gpu": rows, "nq": nq, "hbm_bytes_per_launch": res["hbm_bytes_per_launch"],
-             "source": f"profiles/{rnd}_{tag}_summary.json"}, indent=1))
+             "source": f"profiles/{rnd}_{tag}_summary.json", "csrc_digest": res.get("csrc_digest"),
+             "lib_digest": res.get("lib_digest"), "git_head_at_summary": res.get("git_head_at_summary")},
+            indent=1))
     print(json.dumps(res, indent=1))
 
 

@@ -111,6 +111,8 @@ struct Options {
                              // at nq = 256 (short splits), +0.5-0.9 % on the long splits of (d) and the
                              // N = 8 shard (r5h, r5i, r5k)
     int graph_verbose = 0;   // FX_SEARCH_GRAPH_VERBOSE
+    int scan_v5 = 1;         // FX_SCAN_V5: 16-bit rows of <= 768 B scan with k_scan_v5 (64-row tiles, 256
+                             // queries per workgroup; fx_scan5.hip); 0: k_scan_v4
     int host_spin = 1;       // FX_HOST_SPIN: a host-output search waits for its results by polling the
                              // stream (1) instead of a blocking hipStreamSynchronize (0)
 #ifdef FX_DIAG
@@ -144,6 +146,7 @@ struct Options {
         num("FX_COLD_BOUND", cold_bound);
         num("FX_SEARCH_GRAPH_VERBOSE", graph_verbose);
         num("FX_HOST_SPIN", host_spin);
+        num("FX_SCAN_V5", scan_v5);
         (void)str;
 #ifdef FX_DIAG
         num("FX_FORCE_FALLBACK", force_fallback);
@@ -181,6 +184,7 @@ struct Options {
             {"tight_at", &tight_at, -1, CAP, nullptr, 0},
             {"cold_bound", &cold_bound, -1, 1, nullptr, 0},
             {"host_spin", &host_spin, 0, 1, nullptr, 0},
+            {"scan_v5", &scan_v5, 0, 1, nullptr, 0},
 #ifdef FX_DIAG
             {"force_fallback", &force_fallback, 0, 2, nullptr, 0},
             {"scan_dbg", &scan_dbg, 0, 1 << 20, nullptr, 0},
@@ -368,8 +372,14 @@ int fill_splits(int live_tiles, int eff_tiles, int n_ctiles, int min_tiles) {
 // rows and the certification bound (the smallest full split's KP-th key)
 // lies far beyond the k-th distance
 void plan_scan(const FxIndex* h, int64_t nq, int k, ScanParams& p) {
-    p.n_qtiles = (int)((nq + TILE_Q - 1) / TILE_Q);
-    p.n_ctiles = (int)((h->ntotal + TILE_R - 1) / TILE_R);
+    // the scan's shape: k_scan_v5 (64-row tiles x 256 queries) for the 16-bit
+    // rows it has (not with the key-matrix dump, whose layout is k_scan_v4's)
+    const int sdt = h->img_kind == IMG_F32S ? (int)F32S : h->dtype;
+    const bool v5 = h->opt.scan_v5 != 0 && scan_v5_supports(sdt, h->row_bytes) && !(h->opt.scan_dbg & 32);
+    p.qt = v5 ? V5_QT : TILE_Q;
+    p.tr = v5 ? V5_TR : TILE_R;
+    p.n_qtiles = (int)((nq + p.qt - 1) / p.qt);
+    p.n_ctiles = (int)((h->ntotal + p.tr - 1) / p.tr);
     p.place = 0;
     p.sx = 0;
     p.pub = nullptr;
@@ -429,7 +439,8 @@ void plan_scan(const FxIndex* h, int64_t nq, int k, ScanParams& p) {
     // cold-start bound: pays on short splits, where a block's first record
     // tiles are a large share of its work
     const int cb = h->opt.cold_bound;
-    p.cold_bound = !p.share ? 0 : cb >= 0 ? cb : (nct + p.splits - 1) / p.splits <= 256 ? 1 : 0;
+    p.cold_bound = !p.share ? 0 : cb >= 0 ? cb : ((int64_t)(nct + p.splits - 1) / p.splits) * p.tr <= 256 * TILE_R ? 1 : 0;
+    if (v5) p.tight_at = 0;  // (k_scan_v5 has no between-compaction re-bound)
 }
 
 // k > KP: approx candidates the refine re-ranks exactly (k_refine_big)
@@ -523,9 +534,14 @@ hipError_t update_scan_image(FxIndex* h) {
 // and never sends re-scannable queries to the exact scan.
 hipError_t plan_rescan(FxIndex* h, SearchPlan& P) {
     hipError_t e;
-    const int64_t nq = std::min<int64_t>(P.nq, RESCAN_MAX), nq_pad = round_up(nq, QPAD);
+    const int64_t nq = std::min<int64_t>(P.nq, RESCAN_MAX);
     const int k1 = std::min(2 * FX_BIG_K, std::max(512, 4 * P.k));
     int* n_flag = P.rp.n_flag;
+    ScanParams& sp = P.sp2;
+    sp = P.sp;
+    sp.nq = nq;
+    plan_scan(h, nq, k1, sp);  // k1 > KP: share = 0, >= k1/4 splits
+    const int64_t nq_pad = round_up(nq, std::max<int64_t>(QPAD, sp.qt));
     if ((e = h->rq_f32.ensure((size_t)nq_pad * h->kdim * 4)) != hipSuccess) return e;
     if ((e = h->rq_op.ensure((size_t)nq_pad * h->row_bytes)) != hipSuccess) return e;
     if ((e = h->rq_eps.ensure((size_t)nq * 4)) != hipSuccess) return e;
@@ -549,10 +565,6 @@ hipError_t plan_rescan(FxIndex* h, SearchPlan& P) {
     pp.qeps = (float*)h->rq_eps.p;
     pp.qrho = (float*)h->rq_rho.p;
     pp.qshift = (double*)h->rq_shift.p;
-    ScanParams& sp = P.sp2;
-    sp = P.sp;
-    sp.nq = nq;
-    plan_scan(h, nq, k1, sp);  // k1 > KP: share = 0, >= k1/4 splits
     sp.qop = (const char*)h->rq_op.p;
     sp.gtau = (unsigned*)h->rq_gtau.p;
     sp.pub = nullptr;
@@ -562,7 +574,7 @@ hipError_t plan_rescan(FxIndex* h, SearchPlan& P) {
     sp.dbgbuf = nullptr;
     sp.stamps = nullptr;
     sp.nq_dev = n_flag;
-    const size_t ncand = (size_t)sp.n_qtiles * sp.splits * TILE_Q * KP;
+    const size_t ncand = (size_t)sp.n_qtiles * sp.splits * sp.qt * KP;
     if ((e = h->rq_cand_d.ensure(ncand * 4)) != hipSuccess) return e;
     if ((e = h->rq_cand_i.ensure(ncand * 4)) != hipSuccess) return e;
     sp.cand_d = (float*)h->rq_cand_d.p;
@@ -573,6 +585,7 @@ hipError_t plan_rescan(FxIndex* h, SearchPlan& P) {
     rp.cand_d = sp.cand_d;
     rp.cand_i = sp.cand_i;
     rp.splits = sp.splits;
+    rp.qt = sp.qt;
     rp.qf32 = pp.qf32;
     rp.qeps = pp.qeps;
     rp.qrho = pp.qrho;
@@ -598,8 +611,10 @@ hipError_t plan_search(FxIndex* h, int64_t nq, const void* qdev, int q_dtype, in
     P.nq = nq;
     P.k = k;
     P.q_dtype = q_dtype;
-    P.nq_pad = round_up(nq, QPAD);
     P.scan_dt = h->img_kind == IMG_F32S ? (int)F32S : h->dtype;
+    ScanParams& sp = P.sp;
+    plan_scan(h, nq, k, sp);
+    P.nq_pad = round_up(nq, std::max<int64_t>(QPAD, sp.qt));  // whole scan tiles of (zero) queries
     const bool img = h->img_kind != IMG_NONE;
     if ((e = h->qf32.ensure((size_t)P.nq_pad * h->kdim * 4)) != hipSuccess) return e;
     if ((e = h->qop.ensure((size_t)P.nq_pad * h->row_bytes)) != hipSuccess) return e;
@@ -627,8 +642,6 @@ hipError_t plan_search(FxIndex* h, int64_t nq, const void* qdev, int q_dtype, in
     pp.qidx = nullptr;
     pp.nq_dev = nullptr;
 
-    ScanParams& sp = P.sp;
-    plan_scan(h, nq, k, sp);
     sp.codes = h->img_kind == IMG_F32S ? (const char*)h->split.p : h->codes;
     sp.norms = img ? (const float*)h->cnorms.p : h->norms;
     sp.ntotal = h->ntotal;
@@ -641,7 +654,7 @@ hipError_t plan_search(FxIndex* h, int64_t nq, const void* qdev, int q_dtype, in
     // k_scan_v4's published per-split lists (the union threshold, see
     // compact_wave): slow-path tiles 25.7 -> 16.5 %, config (d) -3 %
     if (sp.share && sp.splits > 1 && h->opt.pub != 0) {
-        const size_t npub = (size_t)sp.n_qtiles * TILE_Q * sp.splits * KP;
+        const size_t npub = (size_t)sp.n_qtiles * sp.qt * sp.splits * KP;
         if ((e = h->pub.ensure(npub * 4)) != hipSuccess) return e;
         sp.pub = (float*)h->pub.p;
         // union bound taken at rank max(6k/5, 12) (<= KP): tighter pruning;
@@ -651,7 +664,7 @@ hipError_t plan_search(FxIndex* h, int64_t nq, const void* qdev, int q_dtype, in
         sp.prune_rank = h->opt.prune_rank > 0 ? h->opt.prune_rank : std::max(6 * k / 5, 12);
         sp.prune_rank = std::max(k, std::min(KP, sp.prune_rank));
     }
-    P.ncand = (size_t)sp.n_qtiles * sp.splits * TILE_Q * KP;
+    P.ncand = (size_t)sp.n_qtiles * sp.splits * sp.qt * KP;
     if ((e = h->cand_d.ensure(P.ncand * 4)) != hipSuccess) return e;
     if ((e = h->cand_i.ensure(P.ncand * 4)) != hipSuccess) return e;
     sp.cand_d = (float*)h->cand_d.p;
@@ -666,6 +679,7 @@ hipError_t plan_search(FxIndex* h, int64_t nq, const void* qdev, int q_dtype, in
     rp.cand_d = sp.cand_d;
     rp.cand_i = sp.cand_i;
     rp.splits = sp.splits;
+    rp.qt = sp.qt;
     rp.nq = nq;
     rp.ntotal = h->ntotal;
     rp.k = k;
@@ -693,7 +707,7 @@ hipError_t plan_search(FxIndex* h, int64_t nq, const void* qdev, int q_dtype, in
     P.reduce = small_many(k, nq, sp.splits) && h->opt.reduce_cand == 2;
     rp.wg = small_many(k, nq, sp.splits) && h->opt.reduce_cand == 1 ? 1 : 0;
     if (P.reduce) {
-        const size_t nred = (size_t)sp.n_qtiles * ((sp.splits + 15) / 16) * TILE_Q * KP;
+        const size_t nred = (size_t)sp.n_qtiles * ((sp.splits + 15) / 16) * sp.qt * KP;
         if ((e = h->cand2_d.ensure(nred * 4)) != hipSuccess) return e;
         if ((e = h->cand2_i.ensure(nred * 4)) != hipSuccess) return e;
     }
@@ -725,7 +739,7 @@ hipError_t enqueue_main(FxIndex* h, SearchPlan& P, hipStream_t s, bool timed, hi
     RefineParams rp = P.rp;
     if (P.reduce) {
         int ng = 0;
-        if ((e = launch_reduce_cand(P.sp.cand_d, P.sp.cand_i, P.sp.splits, P.nq, P.sp.n_qtiles, (float*)h->cand2_d.p,
+        if ((e = launch_reduce_cand(P.sp.cand_d, P.sp.cand_i, P.sp.splits, P.nq, P.sp.qt, (float*)h->cand2_d.p,
                                     (int*)h->cand2_i.p, &ng, P.rp.ntotal, P.rp.n_drop, s)) != hipSuccess)
             return e;
         rp.cand_d = (const float*)h->cand2_d.p;
@@ -895,7 +909,7 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
         HIP_TRY(hipMemsetAsync(h->stamps.p, 0, grid * 4 * 128, s));
         P.sp.stamps = (unsigned long long*)h->stamps.p;
     }
-    const size_t nkeys = (size_t)P.sp.n_qtiles * TILE_Q * P.sp.n_ctiles * TILE_R;
+    const size_t nkeys = (size_t)P.sp.n_qtiles * P.sp.qt * P.sp.n_ctiles * P.sp.tr;
     if ((P.sp.dbg & 32) && nkeys <= (size_t)1 << 26) {
         HIP_TRY(h->dbgbuf.ensure(nkeys * 4));
         HIP_TRY(hipMemsetAsync(h->dbgbuf.p, 0xff, nkeys * 4, s));
@@ -1024,7 +1038,7 @@ std::vector<uint64_t> graph_key(const FxIndex* h, int64_t nq, int q_dtype, int k
             (uint64_t)o.force_fallback, (uint64_t)o.place, (uint64_t)o.sx, (uint64_t)o.reduce_cand,
             (uint64_t)o.pub, (uint64_t)o.prune_rank, (uint64_t)o.compact_at, (uint64_t)o.union_w,
             (uint64_t)o.union_defer, (uint64_t)(int64_t)o.union_inplace, (uint64_t)(int64_t)o.tight_at, (uint64_t)o.cold_bound,
-            (uint64_t)o.reduce_cand,
+            (uint64_t)o.reduce_cand, (uint64_t)o.scan_v5,
             (uint64_t)(uintptr_t)h->codes, (uint64_t)(uintptr_t)h->norms, (uint64_t)(uintptr_t)h->split.p,
             (uint64_t)(uintptr_t)h->cnorms.p, (uint64_t)(uintptr_t)h->centre.p, (uint64_t)(uintptr_t)h->qshift.p,
             (uint64_t)(uintptr_t)h->qin.p, (uint64_t)(uintptr_t)h->qf32.p, (uint64_t)(uintptr_t)h->qop.p,

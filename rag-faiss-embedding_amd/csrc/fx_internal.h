@@ -81,6 +81,9 @@ struct ScanParams {
                                 // past the deferred slots); the rest publish only their own bound
     int cold_bound;             // 1: a still-empty list's first record tile bounds its threshold by the
                                 // prune_rank-th of the tile's group minima before pushing
+    int qt;                     // queries per scan tile (the candidate layout's [qtile][split][qt][KP]):
+                                // TILE_Q (k_scan_v4 / k_scan_topk) or 256 (k_scan_v5)
+    int tr;                     // corpus rows per scan tile: TILE_R, or 64 (k_scan_v5)
 };
 
 // queries are zero-padded to a multiple of QPAD (the scan's query tile)
@@ -116,6 +119,7 @@ struct RefineParams {
     int64_t ntotal;        // rows of the index: a candidate row id outside [0, ntotal) is never gathered
     int* n_drop;           // ... and counted here (ids other than -1 outside [0, ntotal): a corrupted
                            // candidate list), read back by fx_index_last_dropped_candidates
+    int qt;                // queries per scan tile of the candidate layout (ScanParams.qt)
     int wg;                // 1: small batches over many splits (k <= KP): one 16-wave workgroup per query
                            // (k_refine_wg: the waves share the walk over splits * KP candidates); 0: k_refine
 };
@@ -182,8 +186,12 @@ hipError_t launch_scan_mfma(int st_dt, int metric, const ScanParams& p, hipStrea
 hipError_t launch_refine(int st_dt, int metric, const RefineParams& p, hipStream_t s);
 // small batches: merge each 16 splits' candidate lists of a query into their
 // top KP (k_reduce_cand); *ngroups = ceil(splits / 16) lists per query after
-hipError_t launch_reduce_cand(const float* cd, const int* ci, int splits, int64_t nq, int n_qtiles, float* od,
+hipError_t launch_reduce_cand(const float* cd, const int* ci, int splits, int64_t nq, int qt, float* od,
                               int* oi, int* ngroups, int64_t ntotal, int* n_drop, hipStream_t s);
+// fx_scan5.hip: the 64-row-tile, 256-query scan (k_scan_v5) and the shapes it has
+bool scan_v5_supports(int st_dt, int row_bytes);
+hipError_t launch_scan_v5(int st_dt, int metric, const ScanParams& p, hipStream_t s);
+constexpr int V5_QT = 256, V5_TR = 64;
 // both fallback launches, always enqueued; they read the flagged count at
 // n_flag[0] (list at n_flag + 1) and do nothing when it is 0
 hipError_t launch_exact_fallback(int st_dt, int metric, const char* codes, int row_bytes, int kdim,

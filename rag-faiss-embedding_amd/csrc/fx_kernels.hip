@@ -800,13 +800,14 @@ __device__ __forceinline__ void refine_take(float d, int i, float& bd, int& bi, 
 template <int G>
 __global__ __launch_bounds__(256) void k_reduce_cand(const float* __restrict__ cd, const int* __restrict__ ci,
                                                      int splits, int64_t nq, int ngroups, float* __restrict__ od,
-                                                     int* __restrict__ oi, int64_t ntotal, int* __restrict__ n_drop) {
+                                                     int* __restrict__ oi, int64_t ntotal, int* __restrict__ n_drop,
+                                                     int qt) {
     const int lane = threadIdx.x & 63;
     const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int64_t q = w / ngroups;
     const int g = (int)(w - q * ngroups);
     if (q >= nq) return;
-    const int qtile = (int)(q / TILE_Q), qq = (int)(q % TILE_Q);
+    const int qtile = (int)(q / qt), qq = (int)(q % qt);
     const int s0 = g * G, ns = min(G, splits - s0);
     constexpr int NL = G * KP / 64;  // loads per lane
     float dv[NL];
@@ -818,7 +819,7 @@ __global__ __launch_bounds__(256) void k_reduce_cand(const float* __restrict__ c
         dv[u] = FX_INF;
         iv[u] = INT_MAX;
         if (s < ns) {
-            const int64_t off = (((int64_t)qtile * splits + s0 + s) * TILE_Q + qq) * KP + j;
+            const int64_t off = (((int64_t)qtile * splits + s0 + s) * qt + qq) * KP + j;
             const int ii = ci[off];
             const float dd = cd[off];
             if (ii >= 0 && ii < ntotal) { dv[u] = dd; iv[u] = ii; }
@@ -831,7 +832,7 @@ __global__ __launch_bounds__(256) void k_reduce_cand(const float* __restrict__ c
 #pragma unroll
     for (int u = 0; u < NL; ++u) refine_take(dv[u], iv[u], bd, bi, td, ti, nvalid, lane);
     if (lane < KP) {
-        const int64_t o = (((int64_t)qtile * ngroups + g) * TILE_Q + qq) * KP + lane;
+        const int64_t o = (((int64_t)qtile * ngroups + g) * qt + qq) * KP + lane;
         od[o] = bd;
         oi[o] = bi == INT_MAX ? -1 : bi;
     }
@@ -852,14 +853,13 @@ hipError_t launch_rescan_chunks(const int* n_flag, int cap, int nchunks, int* co
     return hipGetLastError();
 }
 
-hipError_t launch_reduce_cand(const float* cd, const int* ci, int splits, int64_t nq, int n_qtiles, float* od,
+hipError_t launch_reduce_cand(const float* cd, const int* ci, int splits, int64_t nq, int qt, float* od,
                               int* oi, int* ngroups, int64_t ntotal, int* n_drop, hipStream_t s) {
     constexpr int G = 16;
     *ngroups = (splits + G - 1) / G;
-    (void)n_qtiles;
     const int64_t waves = nq * (int64_t)*ngroups;
     hipLaunchKernelGGL((k_reduce_cand<G>), dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, cd, ci, splits, nq,
-                       *ngroups, od, oi, ntotal, n_drop);
+                       *ngroups, od, oi, ntotal, n_drop, qt);
     return hipGetLastError();
 }
 
@@ -890,7 +890,7 @@ __global__ __launch_bounds__(256) void k_refine(RefineParams p) {
     const int lane = threadIdx.x & 63;
     const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (q >= p.nq) return;
-    const int qtile = (int)(q / TILE_Q), qq = (int)(q % TILE_Q);
+    const int qtile = (int)(q / p.qt), qq = (int)(q % p.qt);
     const int ncand = p.splits * KP;
 
     // ---- phase 1: KP smallest approx keys over all splits (running best-64)
@@ -908,7 +908,7 @@ __global__ __launch_bounds__(256) void k_refine(RefineParams p) {
                 iv[u] = INT_MAX;
                 if (c < ncand) {
                     const int s = c / KP, j = c - s * KP;
-                    const int64_t off = (((int64_t)qtile * p.splits + s) * TILE_Q + qq) * KP + j;
+                    const int64_t off = (((int64_t)qtile * p.splits + s) * p.qt + qq) * KP + j;
                     const float dd = p.cand_d[off];  // both loads in flight together
                     const int ii = p.cand_i[off];
                     if (ii >= 0 && ii < p.ntotal) { dv[u] = dd; iv[u] = ii; }
@@ -925,7 +925,7 @@ __global__ __launch_bounds__(256) void k_refine(RefineParams p) {
             int i = INT_MAX;
             if (c < ncand) {
                 const int s = c / KP, j = c - s * KP;
-                const int64_t off = (((int64_t)qtile * p.splits + s) * TILE_Q + qq) * KP + j;
+                const int64_t off = (((int64_t)qtile * p.splits + s) * p.qt + qq) * KP + j;
                 const int ii = p.cand_i[off];
                 if (ii >= 0 && ii < p.ntotal) { d = p.cand_d[off]; i = ii; }
                 else bad += cand_id_corrupt(ii, p.ntotal);
@@ -996,9 +996,14 @@ __global__ __launch_bounds__(256) void k_refine(RefineParams p) {
 
 // refine_take for a chunk that is two ascending runs of KP = 32 (lanes 0-31,
 // 32-63): two consecutive splits' lists as the scan flushed them (sorted by
-// (key, row)).  Reversing the upper run makes the chunk bitonic, so a 6-step
-// merge replaces the 21-step sort; a chunk that is not two sorted runs (a
-// corrupted id masked to INT_MAX, -0 against +0 keys) takes the full sort.
+// (key, row)).  Reversing the lower run makes the chunk bitonic, and a 6-step
+// merge sorts it DEscending -- ready to meet the ascending running best
+// lane by lane (the 64 smallest of the union, bitonic) without the reversal
+// merge_into does; the 21-step sort is only for a chunk that is not two
+// sorted runs (a corrupted id masked to INT_MAX, -0 against +0 keys).
+__device__ __forceinline__ void merge64_desc(float& d, int& i, int lane) {  // bitonic -> descending
+    static_for<6>([&](auto T) { cmpx_s<(32 >> decltype(T)::value)>(d, i, lane, false); });
+}
 __device__ __forceinline__ void refine_take2(float d, int i, float& bd, int& bi, float& td, int& ti, int& nvalid,
                                              int lane) {
     nvalid += __popcll(__ballot(i != INT_MAX));
@@ -1007,17 +1012,21 @@ __device__ __forceinline__ void refine_take2(float d, int i, float& bd, int& bi,
     if (!pass) { d = FX_INF; i = INT_MAX; }  // (a suffix of each sorted run)
     const float pd = __shfl(d, lane - 1, 64);
     const int pi = __shfl(i, lane - 1, 64);
-    if (__any((lane & 31) != 0 && key_lt(d, i, pd, pi))) {
-        sort64(d, i, lane);
-    } else {
-        const int src = lane < 32 ? lane : 95 - lane;
+    const bool sorted = !__any((lane & 31) != 0 && key_lt(d, i, pd, pi));
+    if (sorted) {  // [lower run reversed | upper run]: bitonic
+        const int src = lane < 32 ? 31 - lane : lane;
         d = __shfl(d, src, 64);
         i = __shfl(i, src, 64);
-        merge64(d, i, lane);
+        merge64_desc(d, i, lane);
+    } else {
+        sort64(d, i, lane);
+        d = __shfl(d, 63 - lane, 64);
+        i = __shfl(i, 63 - lane, 64);
     }
-    merge_into(bd, bi, d, i, lane);
-    td = __shfl(bd, KP - 1, 64);
-    ti = __shfl(bi, KP - 1, 64);
+    if (key_lt(d, i, bd, bi)) { bd = d; bi = i; }  // ascending best vs descending chunk: bitonic
+    merge64(bd, bi, lane);
+    td = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, bd), KP - 1));
+    ti = __builtin_amdgcn_readlane(bi, KP - 1);
 }
 
 // Small batches over many corpus splits (the reference's one-query call: 192
@@ -1035,7 +1044,7 @@ __device__ __forceinline__ void refine_take2(float d, int i, float& bd, int& bi,
 template <int DT, int METRIC, int NW>
 __global__ __launch_bounds__(64 * NW) void k_refine_wg(RefineParams p) {
     static_assert((NW & (NW - 1)) == 0 && NW >= 2, "pairwise merge tree");
-    constexpr int PF = 4;
+    constexpr int PF = 8;  // chunks of 64 whose loads are in flight together (one round at 256 splits)
     __shared__ float s_d[NW * KP];
     __shared__ int s_i[NW * KP];
     __shared__ int s_nv[NW];
@@ -1043,7 +1052,7 @@ __global__ __launch_bounds__(64 * NW) void k_refine_wg(RefineParams p) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t q = blockIdx.x;
     if (q >= p.nq) return;  // (block-uniform)
-    const int qtile = (int)(q / TILE_Q), qq = (int)(q % TILE_Q);
+    const int qtile = (int)(q / p.qt), qq = (int)(q % p.qt);
     const int ncand = p.splits * KP;
 
     // ---- phase 1: this wave's KP best approx keys over its chunks
@@ -1060,7 +1069,7 @@ __global__ __launch_bounds__(64 * NW) void k_refine_wg(RefineParams p) {
             iv[u] = INT_MAX;
             if (c < ncand) {
                 const int s = c / KP, j = c - s * KP;
-                const int64_t off = (((int64_t)qtile * p.splits + s) * TILE_Q + qq) * KP + j;
+                const int64_t off = (((int64_t)qtile * p.splits + s) * p.qt + qq) * KP + j;
                 const float dd = p.cand_d[off];
                 const int ii = p.cand_i[off];
                 if (ii >= 0 && ii < p.ntotal) { dv[u] = dd; iv[u] = ii; }
@@ -1167,7 +1176,7 @@ __global__ __launch_bounds__(BT_THREADS) void k_refine_big(RefineParams p) {
     if (q >= (p.nq_dev ? min((int64_t)*p.nq_dev, p.nq) : p.nq)) return;
     const int64_t oq = p.out_idx ? (int64_t)p.out_idx[q] : q;  // output row (the re-scan scatters)
     const int tid = threadIdx.x;
-    const int qtile = (int)(q / TILE_Q), qq = (int)(q % TILE_Q);
+    const int qtile = (int)(q / p.qt), qq = (int)(q % p.qt);
     const int K1 = p.k1, B = bt_cap(K1);
     if (tid == 0) t_split = f2ord(FX_INF);
     bt_init(&st);
@@ -1179,7 +1188,7 @@ __global__ __launch_bounds__(BT_THREADS) void k_refine_big(RefineParams p) {
         bool valid = false;
         if (c < ncand) {
             const int s = c / KP, j = c - s * KP;
-            const int64_t off = (((int64_t)qtile * p.splits + s) * TILE_Q + qq) * KP + j;
+            const int64_t off = (((int64_t)qtile * p.splits + s) * p.qt + qq) * KP + j;
             const int ii = p.cand_i[off];
             if (ii >= 0 && ii < p.ntotal) {
                 d = p.cand_d[off];
@@ -1521,6 +1530,8 @@ static hipError_t scan_t(const ScanParams& p, hipStream_t s) {
 }
 
 hipError_t launch_scan(int st_dt, int metric, const ScanParams& p, hipStream_t s) {
+    if (p.tr == V5_TR) return launch_scan_v5(st_dt, metric, p, s);  // (the plan chose k_scan_v5)
+    if (p.qt != TILE_Q || p.tr != TILE_R) return hipErrorInvalidValue;
     // the MFMA scan (fx_scan.hip) covers every row width it has a register
     // layout for; other widths take the generic kernel above
     if (st_dt == F32S) {  // the split-fp32 operand exists only for the MFMA scans

@@ -18,7 +18,7 @@ import pytest
 ROOT = Path(__file__).resolve().parents[1]
 CSRC = ROOT / "rag-faiss-embedding_amd" / "csrc"
 HIPCC = "/opt/rocm/bin/hipcc"
-UNITS = ["fx_scan.hip"]
+UNITS = ["fx_scan.hip", "fx_scan5.hip"]
 
 pytestmark = pytest.mark.skipif(not Path(HIPCC).exists(), reason="hipcc not available")
 
@@ -60,14 +60,14 @@ def test_checker_flags_known_hazards(tmp_path):
 
 @pytest.mark.parametrize("unit", UNITS)
 def test_scan_kernels_use_no_scratch(asm_files, unit):
-    """Every k_scan_v4 instance runs without private (scratch) memory: its
+    """Every k_scan_v4 / k_scan_v5 instance runs without private (scratch) memory: its
     stage waits count the VMEM operations in flight (`s_waitcnt vmcnt(N)` with
     a compile-time N), and a scratch load or store would be one more such
     operation the count does not know about.  (A by-reference lambda capture
     of the kernel's by-value parameters once put them in scratch.)"""
     import re
     text = asm_files[unit].read_text()
-    sizes = re.findall(r"\.name:\s+(_ZN2fx9k_scan_v4\S+)\s+\.private_segment_fixed_size:\s+(\d+)", text)
-    assert sizes, "no k_scan_v4 kernel metadata found"
+    sizes = re.findall(r"\.name:\s+(_ZN2fx\S*k_scan_v[45]\S+)\s+\.private_segment_fixed_size:\s+(\d+)", text)
+    assert sizes, "no k_scan_v4 / k_scan_v5 kernel metadata found"
     bad = [(n, int(v)) for n, v in sizes if int(v) != 0]
     assert not bad, f"scan kernels with scratch: {bad}"

@@ -196,14 +196,23 @@ __device__ __forceinline__ void merge_into(float& bd, Id& bi, float cd, Id ci, i
     merge64(bd, bi, lane);
 }
 
+// butterfly sums with the partner exchange on the VALU (DPP / permlane:
+// lane_xor) instead of ds_bpermute; the same addition order as a
+// __shfl_xor loop over 32, 16, .., 1, so the same result bit for bit
 __device__ __forceinline__ double wave_sum_f64(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    const int lane = __lane_id();
+    static_for<6>([&](auto T) {
+        constexpr int S = 32 >> decltype(T)::value;
+        v += __longlong_as_double(lane_xor<S>((long long)__double_as_longlong(v), lane));
+    });
     return v;
 }
 __device__ __forceinline__ float wave_sum_f32(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    const int lane = __lane_id();
+    static_for<6>([&](auto T) {
+        constexpr int S = 32 >> decltype(T)::value;
+        v += lane_xor<S>(v, lane);
+    });
     return v;
 }
 

@@ -111,8 +111,8 @@ struct Options {
                              // at nq = 256 (short splits), +0.5-0.9 % on the long splits of (d) and the
                              // N = 8 shard (r5h, r5i, r5k)
     int graph_verbose = 0;   // FX_SEARCH_GRAPH_VERBOSE
-    int scan_v5 = 1;         // FX_SCAN_V5: 16-bit rows of <= 768 B scan with k_scan_v5 (64-row tiles, 256
-                             // queries per workgroup; fx_scan5.hip); 0: k_scan_v4
+    int scan_v5 = 1;         // FX_SCAN_V5: 16-bit rows of 512 / 768 / 1,536 B scan with k_scan_v5 (64-row
+                             // tiles, 256 / 192 queries per workgroup; fx_scan5.hip); 0: k_scan_v4
     int host_spin = 1;       // FX_HOST_SPIN: a host-output search waits for its results by polling the
                              // stream (1) instead of a blocking hipStreamSynchronize (0)
 #ifdef FX_DIAG
@@ -375,8 +375,14 @@ void plan_scan(const FxIndex* h, int64_t nq, int k, ScanParams& p) {
     // the scan's shape: k_scan_v5 (64-row tiles x 256 queries) for the 16-bit
     // rows it has (not with the key-matrix dump, whose layout is k_scan_v4's)
     const int sdt = h->img_kind == IMG_F32S ? (int)F32S : h->dtype;
-    const bool v5 = h->opt.scan_v5 != 0 && scan_v5_supports(sdt, h->row_bytes) && !(h->opt.scan_dbg & 32);
-    p.qt = v5 ? V5_QT : TILE_Q;
+    // ... when its wider query tiles add no padding work: v5 query slots within
+    // 5 % of k_scan_v4's (nq = 256 on 1,536-B rows would scan 384 slots for
+    // 256 queries: 5.59 against 3.61 ms, profiles/r6/ab_v5_d_r6e.txt; one-query
+    // calls keep k_scan_v4's 128-query tile)
+    const int v5qt = h->opt.scan_v5 != 0 && !(h->opt.scan_dbg & 32) ? scan_v5_qt(sdt, h->row_bytes) : 0;
+    const int64_t slots4 = (nq + TILE_Q - 1) / TILE_Q * TILE_Q;
+    const bool v5 = v5qt > 0 && (nq + v5qt - 1) / v5qt * v5qt * 20 <= slots4 * 21;
+    p.qt = v5 ? v5qt : TILE_Q;
     p.tr = v5 ? V5_TR : TILE_R;
     p.n_qtiles = (int)((nq + p.qt - 1) / p.qt);
     p.n_ctiles = (int)((h->ntotal + p.tr - 1) / p.tr);

@@ -189,9 +189,9 @@ hipError_t launch_refine(int st_dt, int metric, const RefineParams& p, hipStream
 hipError_t launch_reduce_cand(const float* cd, const int* ci, int splits, int64_t nq, int qt, float* od,
                               int* oi, int* ngroups, int64_t ntotal, int* n_drop, hipStream_t s);
 // fx_scan5.hip: the 64-row-tile, 256-query scan (k_scan_v5) and the shapes it has
-bool scan_v5_supports(int st_dt, int row_bytes);
+int scan_v5_qt(int st_dt, int row_bytes);  // its queries per workgroup for these rows (0: no shape)
 hipError_t launch_scan_v5(int st_dt, int metric, const ScanParams& p, hipStream_t s);
-constexpr int V5_QT = 256, V5_TR = 64;
+constexpr int V5_TR = 64;
 // both fallback launches, always enqueued; they read the flagged count at
 // n_flag[0] (list at n_flag + 1) and do nothing when it is 0
 hipError_t launch_exact_fallback(int st_dt, int metric, const char* codes, int row_bytes, int kdim,

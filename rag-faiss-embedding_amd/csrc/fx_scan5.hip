@@ -1,6 +1,7 @@
 // fx_scan5.hip -- k_scan_v5: the search() scan with 64-row corpus tiles and
-// NB x 16 stationary queries per wave (NB = 4: 64 queries per wave, 256 per
-// workgroup) for rows of <= 768 B (bf16 / fp16 with d <= 384: config (e)).
+// NB x 16 stationary queries per wave: NB = 4 (64 queries per wave, 256 per
+// workgroup) for 16-bit rows of <= 768 B (d <= 384: config (e)), NB = 3 (48
+// per wave, 192 per workgroup) for 1,536-B rows (d = 768: config (d)).
 //
 // Same algorithm and the same per-split top-KP lists as k_scan_v4
 // (fx_scan.hip: the fused MFMA distance GEMM, the LDS-DMA ring, the shared
@@ -17,9 +18,11 @@
 //   * the per-query lists hold LC = 48 entries (256 lists must fit the LDS
 //     beside the ring: 96 KiB of lists + a 40 KiB ring).
 //
-// The B operand (64 queries x K) takes 48 AGPRs per K-step pair ... = 192
-// AGPRs at K = 384 (KSTEPS = 12), the same as k_scan_v4's 32 queries at
-// K = 768; wider rows stay on k_scan_v4.
+// The B operand takes 4 NB registers per K-step: 192 AGPRs for NB = 4 at
+// K = 384 (KSTEPS = 12) -- k_scan_v4's 32 queries at K = 768 take as many --
+// and 288 for NB = 3 at K = 768, so the third block's upper K-steps live in
+// VGPRs (ODD_KA).  At NB = 3 the ratios are two thirds of k_scan_v4's (an A
+// fragment feeds three MFMAs; 192 queries per 64-row tile).
 #include "fx_scan_common.h"
 
 namespace fx {
@@ -249,16 +252,43 @@ __device__ __forceinline__ float min4_raw(float a, float b, float c, float d) {
     return r;
 }
 
+// One MFMA of the odd query block (NB = 3) with its B fragment in an AGPR
+// (AG) or a VGPR: 72 B fragments at K = 768 (288 registers) do not fit the
+// 256 AGPRs, so the last block's upper K-steps live in VGPRs.
+template <int DT, int INIT, bool AG>
+__device__ __forceinline__ void mma1(f32x4& c, const typename AsmMmaV<DT>::A& a, const typename AsmMmaV<DT>::B& b,
+                                     const f32x4& ci) {
+#define FX_M1(OP)                                                                                              \
+    if constexpr (AG) {                                                                                        \
+        if constexpr (INIT == 0) asm volatile(OP " %0, %1, %2, %0" : "+v"(c) : "v"(a), "a"(b));                \
+        else if constexpr (INIT == 1) asm volatile(OP " %0, %1, %2, %3" : "+v"(c) : "v"(a), "a"(b), "v"(ci)); \
+        else asm volatile(OP " %0, %1, %2, 0" : "+v"(c) : "v"(a), "a"(b));                                     \
+    } else {                                                                                                   \
+        if constexpr (INIT == 0) asm volatile(OP " %0, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b));                \
+        else if constexpr (INIT == 1) asm volatile(OP " %0, %1, %2, %3" : "+v"(c) : "v"(a), "v"(b), "v"(ci)); \
+        else asm volatile(OP " %0, %1, %2, 0" : "+v"(c) : "v"(a), "v"(b));                                     \
+    }
+    if constexpr (DT == F16) {
+        FX_M1("v_mfma_f32_16x16x32_f16")
+    } else {
+        FX_M1("v_mfma_f32_16x16x32_bf16")
+    }
+#undef FX_M1
+}
+// K-steps of the odd query block whose B fragments sit in AGPRs (the rest in
+// VGPRs): 192 + 4 KA <= 256 AGPRs
+constexpr int ODD_KA = 14;
+
 // MFMAs of one A fragment against NB query blocks (pairs through
-// AsmMmaV::mma2: B pinned in AGPRs)
-template <int DT, int INIT, int NB>
+// AsmMmaV::mma2: B pinned in AGPRs; an odd last block through mma1)
+template <int DT, int INIT, int NB, int KS>
 __device__ __forceinline__ void mma_row(f32x4 (&acc)[NB], const typename AsmMmaV<DT>::A& a,
                                         const typename AsmMmaV<DT>::B (&b)[NB], const f32x4& ci) {
-    static_assert(NB % 2 == 0, "query blocks are issued in pairs");
     static_for<NB / 2>([&](auto P) {
         constexpr int n = 2 * decltype(P)::value;
         AsmMmaV<DT>::template mma2<INIT>(acc[n], acc[n + 1], a, b[n], b[n + 1], ci);
     });
+    if constexpr (NB % 2) mma1<DT, INIT, (KS < ODD_KA)>(acc[NB - 1], a, b[NB - 1], ci);
 }
 
 constexpr int RESCAN = 4096;  // (kernel name of the re-scan's instance, as in fx_scan.hip)
@@ -311,10 +341,14 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v5(ScanParams p) {
         for (int ks = 0; ks < KSTEPS; ++ks)
 #pragma unroll
             for (int n = 0; n < NB; ++n) b[ks][n] = *(const bfrag_t*)(qb + n * 16 * RB + ks * 64);
-#pragma unroll
-        for (int ks = 0; ks < KSTEPS; ++ks)
-#pragma unroll
-            for (int n = 0; n < NB; ++n) AsmMmaV<DT>::settle(b[ks][n]);
+        static_for<KSTEPS>([&](auto KS) {
+            constexpr int ks = decltype(KS)::value;
+            static_for<NB>([&](auto N) {
+                constexpr int n = decltype(N)::value;
+                if constexpr (NB % 2 && n == NB - 1 && ks >= ODD_KA) asm volatile("" ::"v"(b[ks][n]));
+                else AsmMmaV<DT>::settle(b[ks][n]);
+            });
+        });
     }
 
     // ---- DMA addressing: piece w of a wave = rows 16 wave + 8 w .. +7 of the
@@ -418,7 +452,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v5(ScanParams p) {
             static_for<M>([&](auto MM) {
                 constexpr int m = decltype(MM)::value;
                 constexpr int INIT = j == 0 ? (METRIC == L2 ? 1 : 2) : 0;
-                mma_row<DT, INIT, NB>(acc[m], X[m], b[kq0], yin[m]);
+                mma_row<DT, INIT, NB, kq0>(acc[m], X[m], b[kq0], yin[m]);
                 if constexpr (m < M / 2) {
                     const uint32_t rd1 = rd_addr + rd_h1;
                     ds_rd128<(2 * m) * 2048>(Y[2 * m], rd1);
@@ -447,7 +481,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v5(ScanParams p) {
             const uint32_t rd_next = lds_base + L::RING_OFF + c1 * S_STAGE + rd_lane;
             static_for<M>([&](auto MM) {
                 constexpr int m = decltype(MM)::value;
-                mma_row<DT, 0, NB>(acc[m], Y[m], b[kq0 + 1], yin[m]);
+                mma_row<DT, 0, NB, kq0 + 1>(acc[m], Y[m], b[kq0 + 1], yin[m]);
                 if constexpr (m < M / 2) {
                     ds_rd128<(2 * m) * 2048>(X[2 * m], rd_next);
                     ds_rd128<(2 * m + 1) * 2048>(X[2 * m + 1], rd_next);
@@ -466,7 +500,11 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v5(ScanParams p) {
         for (int m = 0; m < M; ++m)
 #pragma unroll
             for (int n = 0; n < NB; ++n) gmin[n][m] = min4(acc[m][n]);
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(gr[0]), "+v"(gr[1]), "+v"(gr[NB - 2]), "+v"(gr[NB - 1])::"memory");
+        // (the thresholds as operands: no use of them is scheduled above the wait)
+        if constexpr (NB == 4)
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(gr[0]), "+v"(gr[1]), "+v"(gr[2]), "+v"(gr[3])::"memory");
+        else
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(gr[0]), "+v"(gr[1]), "+v"(gr[NB - 1])::"memory");
         float tn[NB], mn[NB];
 #pragma unroll
         for (int n = 0; n < NB; ++n) {
@@ -627,20 +665,26 @@ static hipError_t rows(const ScanParams& p, hipStream_t s) {
         case 8: return p.nq_dev ? launch_t<DT, METRIC, 8, 4, 48, RESCAN>(p, s) : launch_t<DT, METRIC, 8, 4, 48, 0>(p, s);
         case 12:
             return p.nq_dev ? launch_t<DT, METRIC, 12, 4, 48, RESCAN>(p, s) : launch_t<DT, METRIC, 12, 4, 48, 0>(p, s);
+        case 24:
+            return p.nq_dev ? launch_t<DT, METRIC, 24, 3, 64, RESCAN>(p, s) : launch_t<DT, METRIC, 24, 3, 64, 0>(p, s);
         default: return hipErrorInvalidValue;
     }
 }
 
 }  // namespace v5
 
-// k_scan_v5's shapes: 16-bit rows of 512 or 768 B (d <= 256 / 384), 256
-// queries per workgroup (ScanParams.qt), 64-row tiles (ScanParams.tr)
-bool scan_v5_supports(int st_dt, int row_bytes) {
-    return (st_dt == BF16 || st_dt == F16) && (row_bytes == 512 || row_bytes == 768);
+// k_scan_v5's shapes (ScanParams.qt queries per workgroup, 64-row tiles):
+// 16-bit rows of 512 or 768 B (d <= 256 / 384): 4 query blocks per wave, 256
+// queries; of 1,536 B (d = 768, config (d)): 3 blocks, 192 queries.  0: none.
+int scan_v5_qt(int st_dt, int row_bytes) {
+    if (st_dt != BF16 && st_dt != F16) return 0;
+    if (row_bytes == 512 || row_bytes == 768) return v5::Lds<4, 48>::QT;
+    if (row_bytes == 1536) return v5::Lds<3, 64>::QT;
+    return 0;
 }
 
 hipError_t launch_scan_v5(int st_dt, int metric, const ScanParams& p, hipStream_t s) {
-    if (!scan_v5_supports(st_dt, p.row_bytes) || p.qt != v5::Lds<4, 48>::QT || p.tr != v5::TR)
+    if (scan_v5_qt(st_dt, p.row_bytes) == 0 || p.qt != scan_v5_qt(st_dt, p.row_bytes) || p.tr != v5::TR)
         return hipErrorInvalidValue;
     if (metric == L2) return st_dt == BF16 ? v5::rows<BF16, L2>(p, s) : v5::rows<F16, L2>(p, s);
     return st_dt == BF16 ? v5::rows<BF16, IP>(p, s) : v5::rows<F16, IP>(p, s);

@@ -161,9 +161,9 @@ class _FlatIndex:
                 a.flags.c_contiguous and a.flags.writeable, \
                 f"{name} must be a writeable C-contiguous {np.dtype(dt).name} array of shape ({nq}, {k})"
         self._bind_stream(False)
-        self._check(self._lib.fx_index_search(self._h, nq, x.ctypes.data_as(ctypes.c_void_p), _lib.F32,
-                                              _lib.MEM_HOST, k, Dh.ctypes.data_as(ctypes.c_void_p),
-                                              Ih.ctypes.data_as(ctypes.c_void_p), _lib.MEM_HOST))
+        # (raw addresses: .ctypes.data is an int, much cheaper per call than data_as)
+        self._check(self._lib.fx_index_search(self._h, nq, x.ctypes.data, _lib.F32, _lib.MEM_HOST, k,
+                                              Dh.ctypes.data, Ih.ctypes.data, _lib.MEM_HOST))
         return Dh, Ih
 
     def last_fallbacks(self) -> int:

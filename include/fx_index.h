@@ -93,7 +93,7 @@ int fx_index_set_stream(FxIndex* index, void* stream);
 /* Per-index tuning option (name -> integer value).  Initial
  * values come from the FX_* environment variables, read once at index
  * creation; nothing on the search path reads the environment.  Names and
- * accepted values: "search_graph" 0/1 (default 1: replay small host searches
+ * accepted values: "search_graph" 0/1 (default 0; 1: replay small host searches
  * as one hipGraph), "scan_place" -1/0/1, "scan_sx" >= 0, "reduce_cand" 0/1/2 (small
  * batches over many splits: 1, the default, one 16-wave workgroup refine per
  * query; 2 a separate merge of 16 splits' lists first; 0 neither),

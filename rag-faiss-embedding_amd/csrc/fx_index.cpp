@@ -85,8 +85,10 @@ inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 // Test hooks and diagnostic dumps exist only in the diagnostic build
 // (-DFX_DIAG: libfx_index_diag.so, make diag / abl), never in libfx_index.so.
 struct Options {
-    int search_graph = 1;    // FX_SEARCH_GRAPH: replay small host searches as one hipGraph (round 5:
-                             // on by default, one-query call -7 % on a 100k x 384 fp32 index, r5r)
+    int search_graph = 0;    // FX_SEARCH_GRAPH: replay small host searches as one hipGraph (round 5: -7 %
+                             // per one-query call, r5r; off since round 6: with the call down to three
+                             // kernels and one packed copy, the eager enqueue is 3-7 % faster: 97-101 vs
+                             // 104 us on a 100k x 384 fp32 index, profiles/r6/latency_graph_r6f.jsonl)
     int place = -1;          // FX_SCAN_PLACE: scan block placement (-1 automatic, 0, 1)
     int sx = 0;              // FX_SCAN_SX: corpus splits per XCD under placement 1 (0 automatic)
     int reduce_cand = 1;     // FX_REDUCE_CAND: small nq over many splits: 1 one 16-wave workgroup refine per

@@ -134,3 +134,28 @@ def test_merge_topk_matches_global():
     Dm, Im = F.merge_topk([p[0] for p in parts], [p[1] for p in parts], 10)
     np.testing.assert_array_equal(Im, I)
     np.testing.assert_array_equal(Dm, D)
+
+
+@pytest.mark.parametrize("d,nb,nq", [(768, 20_000, 9), (384, 30_001, 13), (100, 5_003, 7), (7, 1_000, 3)])
+def test_synth_oracle_integer_path_is_exact(d, nb, nq):
+    """flat_l2.c fxo_knn_exact_synth: grid-valued queries take the integer
+    path (exact 4096 * sum (x - y)^2, rounded to fp32 once); it must equal the
+    fp64 restatement bit for bit (ids and distances), including the
+    zero-padded tails of d not a multiple of 16 and partial 4-row blocks."""
+    xq = F.synth(4321, 0, nq, d)
+    D1, I1 = C.knn_exact_synth(1234, nb, d, xq, 10)
+    D2, I2 = C.knn_exact_synth(1234, nb, d, xq, 10, f64=True)
+    np.testing.assert_array_equal(I1, I2)
+    np.testing.assert_array_equal(D1, D2)
+    # and against the numpy restatement on the materialised rows
+    Dr, Ir = F.knn_exact(xq, F.synth(1234, 0, nb, d), 10)
+    np.testing.assert_array_equal(I1, Ir)
+    np.testing.assert_array_equal(D1, Dr)
+
+
+def test_synth_oracle_off_grid_queries_take_fp64():
+    xq = F.synth(4321, 0, 5, 64) + np.float32(1e-3)  # not multiples of 1/64
+    D1, I1 = C.knn_exact_synth(1234, 3_000, 64, xq, 10)
+    D2, I2 = C.knn_exact_synth(1234, 3_000, 64, xq, 10, f64=True)
+    np.testing.assert_array_equal(I1, I2)
+    np.testing.assert_array_equal(D1, D2)

@@ -3,8 +3,10 @@ results out -- the reference's FAISSVectorStore.search call form
 (faiss_store.py:57-77) -- through one captured hipGraph per shape.
 
 Every replay must equal the oracle; the graph must be rebuilt whenever the
-index or the shape changes (add, reset, another k or nq).  The graph holds the
-device-gated exact fallback too (FX_FORCE_FALLBACK=1 case).
+index or the shape changes (add, reset, another k or nq).  The graph holds
+the H2D copy, the three kernels and the packed D2H; a replay whose copy
+reports uncertified queries runs their fallback chain eagerly right after
+(FX_FORCE_FALLBACK=1 case).
 """
 import numpy as np
 import pytest
@@ -24,8 +26,8 @@ def fx():
 
 
 def test_eager_small_search_equals_graph(fx, monkeypatch):
-    """search_graph is on by default: the eager path (FX_SEARCH_GRAPH=0)
-    stays covered and returns the replay's results exactly."""
+    """The eager path (FX_SEARCH_GRAPH=0, the default since round 6) and the
+    replay return the same results exactly."""
     rng = np.random.default_rng(12)
     xb = rng.standard_normal((10_000, 384)).astype(np.float32)
     q = rng.standard_normal((3, 384)).astype(np.float32)

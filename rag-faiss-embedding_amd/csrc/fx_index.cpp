@@ -293,6 +293,8 @@ struct FxIndex {
     DevBuf hout;
     char* hpin = nullptr;
     size_t hpin_bytes = 0;
+    char* qpin = nullptr;   // pinned staging of a host-output search's host queries (<= QPIN_MAX)
+    size_t qpin_bytes = 0;
     int64_t last_fallbacks = 0;
     // uncertified count of the last search, copied stream-ordered into pinned
     // memory; read (after a stream sync) only when asked for (fb_pending)
@@ -880,6 +882,12 @@ int finish_host_out(FxIndex* h, SearchPlan& P, const HostOut& L, char* pin, floa
     return h->last_dropped > 0 ? integrity_error(h) : FX_OK;
 }
 
+// host queries of a host-output search up to this size go through pinned
+// staging (a memcpy and an async DMA instead of the runtime's pageable path:
+// the one-query call is latency bound); the call waits for its results, so
+// the staging buffer is free again when it returns
+constexpr size_t QPIN_MAX = (size_t)4 << 20;
+
 int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int k, float* D, int64_t* I,
               int out_mem) {
     hipStream_t s = h->stream();
@@ -887,8 +895,14 @@ int do_search(FxIndex* h, int64_t nq, const void* q, int q_dtype, int q_mem, int
     // queries -> device
     const void* qdev = q;
     if (q_mem == FX_MEM_HOST) {
-        HIP_TRY(h->qin.ensure((size_t)nq * h->d * qes));
-        HIP_TRY(hipMemcpyAsync(h->qin.p, q, (size_t)nq * h->d * qes, hipMemcpyHostToDevice, s));
+        const size_t qb = (size_t)nq * h->d * qes;
+        HIP_TRY(h->qin.ensure(qb));
+        if (out_mem == FX_MEM_HOST && qb <= QPIN_MAX && ensure_pinned(h->qpin, h->qpin_bytes, qb) == hipSuccess) {
+            memcpy(h->qpin, q, qb);
+            HIP_TRY(hipMemcpyAsync(h->qin.p, h->qpin, qb, hipMemcpyHostToDevice, s));
+        } else {
+            HIP_TRY(hipMemcpyAsync(h->qin.p, q, qb, hipMemcpyHostToDevice, s));
+        }
         qdev = h->qin.p;
     }
     // host results: the packed output buffer (host_out_layout)
@@ -1216,6 +1230,7 @@ void fx_index_free(FxIndex* h) {
         if (h->ghq) (void)hipHostFree(h->ghq);
         if (h->ghout) (void)hipHostFree(h->ghout);
         if (h->hpin) (void)hipHostFree(h->hpin);
+        if (h->qpin) (void)hipHostFree(h->qpin);
         if (h->pin_nf) (void)hipHostFree(h->pin_nf);
         for (auto& pr : h->ev_scan) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
         for (auto& pr : h->ev_merge) (void)hipEventDestroy(pr.second);

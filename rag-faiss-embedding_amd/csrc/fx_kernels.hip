@@ -472,6 +472,9 @@ __global__ __launch_bounds__(256) void k_prep_queries(PrepParams p, double gamma
     const int64_t nq = p.nq_dev ? min((int64_t)*p.nq_dev, p.nq) : p.nq;
     const bool live = r < nq;
     const int64_t src = live && p.qidx ? (int64_t)p.qidx[r] : r;  // source row of q
+    // the index-wide bound terms, fetched before the row's loop (one memory
+    // round trip less on the one-query path)
+    const unsigned mbits = *p.mbits, img_bits = *p.img_bits;
     const int kdim = p.kdim;
     const float scale = p.metric == L2 ? -2.0f : -1.0f;
     // xn2 |x|^2, sc |x - mu|^2 (F32S), on2 |op|^2, rr |r|^2, rx r.x, mn2 |mu|^2
@@ -517,8 +520,8 @@ __global__ __launch_bounds__(256) void k_prep_queries(PrepParams p, double gamma
     const double u = 5.9604644775390625e-8;  // 2^-24
     // M: the largest stored-row norm; Smax: the largest srcC of the scan image
     // (both read on the device: add() never waits for the host to learn them)
-    const double M = sqrt((double)__uint_as_float(*p.mbits));
-    const double Smax = (double)__uint_as_float(*p.img_bits);
+    const double M = sqrt((double)__uint_as_float(mbits));
+    const double Smax = (double)__uint_as_float(img_bits);
     const double on = sqrt(on2);
     double eps, shift = 0.0, rho = 0.0;
     if (p.st_dt == F32S) {
@@ -869,9 +872,9 @@ hipError_t launch_reduce_cand(const float* cd, const int* ci, int splits, int64_
 // sqrt(D) >= sqrt(rho^2 + T) - rho = T / (sqrt(rho^2 + T) + rho) (rho = 0:
 // D >= T, which is also the IP form).  The top-k is exact when the k-th
 // exact key, plus 2 ulp for its own fp32 rounding, lies below that.
-__device__ __forceinline__ bool certified(float kth, float tb, const RefineParams& p, int64_t q) {
-    const double T = (double)tb + p.qshift[q] - (double)p.qeps[q];
-    const double rho = (double)p.qrho[q];
+__device__ __forceinline__ bool certified_v(float kth, float tb, double shift, float eps, float rho_f) {
+    const double T = (double)tb + shift - (double)eps;
+    const double rho = (double)rho_f;
     double dmin = T;
     if (rho > 0.0) {
         const double t = T > 0.0 ? T : 0.0;
@@ -880,6 +883,9 @@ __device__ __forceinline__ bool certified(float kth, float tb, const RefineParam
     }
     const double kup = (double)kth + fabs((double)kth) * 2.384185791015625e-7;  // + 2 ulp
     return kup < dmin;
+}
+__device__ __forceinline__ bool certified(float kth, float tb, const RefineParams& p, int64_t q) {
+    return certified_v(kth, tb, p.qshift[q], p.qeps[q], p.qrho[q]);
 }
 
 // PF = chunks of 64 candidates whose loads are issued together in phase 1
@@ -1041,6 +1047,7 @@ __device__ __forceinline__ void refine_take2(float d, int i, float& bd, int& bi,
 // key td and the candidate count are k_refine's; the exact re-rank of the KP
 // rows is spread over the waves, and wave 0 orders, writes and certifies
 // exactly as k_refine does.
+constexpr int RWG_XQ_MAX = 4096;  // k_refine_wg keeps queries of up to this many dims in LDS
 template <int DT, int METRIC, int NW>
 __global__ __launch_bounds__(64 * NW) void k_refine_wg(RefineParams p) {
     static_assert((NW & (NW - 1)) == 0 && NW >= 2, "pairwise merge tree");
@@ -1049,11 +1056,21 @@ __global__ __launch_bounds__(64 * NW) void k_refine_wg(RefineParams p) {
     __shared__ int s_i[NW * KP];
     __shared__ int s_nv[NW];
     __shared__ double s_ex[KP];
+    __shared__ float s_xq[RWG_XQ_MAX];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t q = blockIdx.x;
     if (q >= p.nq) return;  // (block-uniform)
     const int qtile = (int)(q / p.qt), qq = (int)(q % p.qt);
     const int ncand = p.splits * KP;
+    // everything that does not depend on the selection is fetched now, beside
+    // phase 1's loads (the kernel is a chain of memory round trips): the fp32
+    // query into LDS for phase 2, the certification terms for phase 3
+    const bool xq_lds = p.kdim <= RWG_XQ_MAX;
+    if (xq_lds)
+        for (int c = threadIdx.x; c < p.kdim; c += 64 * NW) s_xq[c] = p.qf32[q * (int64_t)p.kdim + c];
+    const unsigned gq = p.gtau ? p.gtau[q] : 0xff800000u;
+    const double c_shift = p.qshift[q];
+    const float c_eps = p.qeps[q], c_rho = p.qrho[q];
 
     // ---- phase 1: this wave's KP best approx keys over its chunks
     float bd = FX_INF, td = FX_INF;
@@ -1111,7 +1128,7 @@ __global__ __launch_bounds__(64 * NW) void k_refine_wg(RefineParams p) {
 
     // ---- phase 2: exact fp64 values of the KP selected rows (16 lanes / row,
     // 4 rows per wave-step; step r on wave r % NW)
-    const float* xq = p.qf32 + q * (int64_t)p.kdim;
+    const float* xq = xq_lds ? (const float*)s_xq : p.qf32 + q * (int64_t)p.kdim;
     const int grp = lane >> 4, sub = lane & 15;
     for (int r = w; r < KP / 4; r += NW) {
         const int row = __shfl(bi, r * 4 + grp, 64);
@@ -1138,11 +1155,10 @@ __global__ __launch_bounds__(64 * NW) void k_refine_wg(RefineParams p) {
         p.D[q * p.k + lane] = valid ? (METRIC == L2 ? key : -key) : (METRIC == L2 ? FLT_MAX : -FLT_MAX);
         p.I[q * p.k + lane] = valid ? (int64_t)id + p.id_offset : (int64_t)-1;
     }
-    const unsigned gq = p.gtau ? p.gtau[q] : 0xff800000u;  // (k_refine: certify when anything pruned)
-    if (nvalid >= KP || gq < 0xff800000u) {
+    if (nvalid >= KP || gq < 0xff800000u) {  // (k_refine: certify when anything pruned)
         const float kth = __shfl(key, p.k - 1, 64);
         const float tb = p.gtau ? fminf(td, ord2f(gq)) : td;
-        if (!certified(kth, tb, p, q) && lane == 0 && !p.force_fb) {
+        if (!certified_v(kth, tb, c_shift, c_eps, c_rho) && lane == 0 && !p.force_fb) {
             const int pos = atomicAdd(p.n_flag, 1);
             p.flag_list[pos] = (int)q;
         }

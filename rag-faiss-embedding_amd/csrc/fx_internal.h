@@ -84,6 +84,7 @@ struct ScanParams {
     int qt;                     // queries per scan tile (the candidate layout's [qtile][split][qt][KP]):
                                 // TILE_Q (k_scan_v4 / k_scan_topk) or 256 (k_scan_v5)
     int tr;                     // corpus rows per scan tile: TILE_R, or 64 (k_scan_v5)
+    int small_ok;               // 1: nq <= 16 may take k_scan_v4's small-batch instance (option small_scan)
 };
 
 // queries are zero-padded to a multiple of QPAD (the scan's query tile)
@@ -120,10 +121,11 @@ struct RefineParams {
     int* n_drop;           // ... and counted here (ids other than -1 outside [0, ntotal): a corrupted
                            // candidate list), read back by fx_index_last_dropped_candidates
     int qt;                // queries per scan tile of the candidate layout (ScanParams.qt)
-    int wg;                // 1: small batches over many splits (k <= KP): one 16-wave workgroup per query
+    int wg;                // > 0: small batches over many splits (k <= KP): one workgroup of wg (4, 8, 16) waves per query
                            // (k_refine_wg: the waves share the walk over splits * KP candidates); 0: k_refine
 };
-// waves of k_refine_wg's workgroup (one query per workgroup)
+// waves of k_refine_wg's workgroup (one query per workgroup) unless the
+// index's option refine_waves says otherwise (4, 8 or 16)
 constexpr int REFINE_WG_WAVES = 16;
 
 // exact fallback (k_fb_scan / k_fb_merge): corpus splits per flagged query,

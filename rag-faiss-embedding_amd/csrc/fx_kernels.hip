@@ -1574,9 +1574,12 @@ template <int DT, int METRIC>
 static hipError_t refine_t(const RefineParams& p, hipStream_t s) {
     if (p.k > KP || p.k1 > 0)  // (k1 > 0 with k <= KP: the re-scan's wide candidate set)
         hipLaunchKernelGGL((k_refine_big<DT, METRIC>), dim3((unsigned)p.nq), dim3(BT_THREADS), 0, s, p);
+    else if (p.wg == 4)
+        hipLaunchKernelGGL((k_refine_wg<DT, METRIC, 4>), dim3((unsigned)p.nq), dim3(64 * 4), 0, s, p);
+    else if (p.wg == 8)
+        hipLaunchKernelGGL((k_refine_wg<DT, METRIC, 8>), dim3((unsigned)p.nq), dim3(64 * 8), 0, s, p);
     else if (p.wg)
-        hipLaunchKernelGGL((k_refine_wg<DT, METRIC, REFINE_WG_WAVES>), dim3((unsigned)p.nq), dim3(64 * REFINE_WG_WAVES),
-                           0, s, p);
+        hipLaunchKernelGGL((k_refine_wg<DT, METRIC, 16>), dim3((unsigned)p.nq), dim3(64 * 16), 0, s, p);
     else if (p.prefetch > 1)
         hipLaunchKernelGGL((k_refine<DT, METRIC, 4>), dim3((unsigned)((p.nq + 3) / 4)), dim3(256), 0, s, p);
     else

@@ -252,29 +252,6 @@ __device__ __forceinline__ float min4_raw(float a, float b, float c, float d) {
     return r;
 }
 
-// One MFMA of the odd query block (NB = 3) with its B fragment in an AGPR
-// (AG) or a VGPR: 72 B fragments at K = 768 (288 registers) do not fit the
-// 256 AGPRs, so the last block's upper K-steps live in VGPRs.
-template <int DT, int INIT, bool AG>
-__device__ __forceinline__ void mma1(f32x4& c, const typename AsmMmaV<DT>::A& a, const typename AsmMmaV<DT>::B& b,
-                                     const f32x4& ci) {
-#define FX_M1(OP)                                                                                              \
-    if constexpr (AG) {                                                                                        \
-        if constexpr (INIT == 0) asm volatile(OP " %0, %1, %2, %0" : "+v"(c) : "v"(a), "a"(b));                \
-        else if constexpr (INIT == 1) asm volatile(OP " %0, %1, %2, %3" : "+v"(c) : "v"(a), "a"(b), "v"(ci)); \
-        else asm volatile(OP " %0, %1, %2, 0" : "+v"(c) : "v"(a), "a"(b));                                     \
-    } else {                                                                                                   \
-        if constexpr (INIT == 0) asm volatile(OP " %0, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b));                \
-        else if constexpr (INIT == 1) asm volatile(OP " %0, %1, %2, %3" : "+v"(c) : "v"(a), "v"(b), "v"(ci)); \
-        else asm volatile(OP " %0, %1, %2, 0" : "+v"(c) : "v"(a), "v"(b));                                     \
-    }
-    if constexpr (DT == F16) {
-        FX_M1("v_mfma_f32_16x16x32_f16")
-    } else {
-        FX_M1("v_mfma_f32_16x16x32_bf16")
-    }
-#undef FX_M1
-}
 // K-steps of the odd query block whose B fragments sit in AGPRs (the rest in
 // VGPRs): 192 + 4 KA <= 256 AGPRs
 constexpr int ODD_KA = 14;

@@ -426,6 +426,29 @@ __device__ __forceinline__ void tighten_list(const float* lst_d, ListRegs& r, in
     if (gtq && lane == 0) gmin_u32(gtq + qi, hi);
 }
 
+// One MFMA of one query block with its B fragment in an AGPR (AG) or a VGPR:
+// k_scan_v5's odd third block (72 B fragments at K = 768 do not fit the 256
+// AGPRs) and k_scan_v4's one-live-block small batches.
+template <int DT, int INIT, bool AG>
+__device__ __forceinline__ void mma1(f32x4& c, const typename AsmMmaV<DT>::A& a, const typename AsmMmaV<DT>::B& b,
+                                     const f32x4& ci) {
+#define FX_M1(OP)                                                                                              \
+    if constexpr (AG) {                                                                                        \
+        if constexpr (INIT == 0) asm volatile(OP " %0, %1, %2, %0" : "+v"(c) : "v"(a), "a"(b));                \
+        else if constexpr (INIT == 1) asm volatile(OP " %0, %1, %2, %3" : "+v"(c) : "v"(a), "a"(b), "v"(ci)); \
+        else asm volatile(OP " %0, %1, %2, 0" : "+v"(c) : "v"(a), "a"(b));                                     \
+    } else {                                                                                                   \
+        if constexpr (INIT == 0) asm volatile(OP " %0, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b));                \
+        else if constexpr (INIT == 1) asm volatile(OP " %0, %1, %2, %3" : "+v"(c) : "v"(a), "v"(b), "v"(ci)); \
+        else asm volatile(OP " %0, %1, %2, 0" : "+v"(c) : "v"(a), "v"(b));                                     \
+    }
+    if constexpr (DT == F16) {
+        FX_M1("v_mfma_f32_16x16x32_f16")
+    } else {
+        FX_M1("v_mfma_f32_16x16x32_bf16")
+    }
+#undef FX_M1
+}
 // minima without fminf's operand canonicalisation (a v_max per operand: the
 // compiler cannot see that asm results are canonical)
 __device__ __forceinline__ float min_raw(float a, float b) {

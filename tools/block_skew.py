@@ -69,7 +69,7 @@ def run_trace(cfg, nq_override, path):
     return rows, d, dtype, nq, row_bytes, wall
 
 
-def model(tr, rows, row_bytes, R_list, dt_tiles=2.0):
+def model(tr, rows, row_bytes, R_list, dt_tiles=2.0, tile_rows=128):
     xcc = (tr[:, 0] & 0xF).astype(np.int64)
     cu = ((tr[:, 0] >> 8) >> 8 & 0xFF).astype(np.int64) + 256 * xcc
     split = tr[:, 1].astype(np.int64)
@@ -78,12 +78,12 @@ def model(tr, rows, row_bytes, R_list, dt_tiles=2.0):
     ok = (tr[:, 2] > 0) & (tr[:, 3] > tr[:, 2])
     xcc, cu, split, t0, t1 = xcc[ok], cu[ok], split[ok], t0[ok], t1[ok]
     nsplit = int(split.max()) + 1
-    n_ct = (rows + 127) // 128
+    n_ct = (rows + tile_rows - 1) // tile_rows
     ntiles = np.array([(s + 1) * n_ct // nsplit - s * n_ct // nsplit for s in range(nsplit)])[split]
     tile_t = (t1 - t0) / np.maximum(ntiles, 1)
     T0, T1 = t0.min(), t1.max()
     dt = float(np.median(tile_t)) * dt_tiles
-    tile_bytes = 128 * row_bytes + 128 * 4  # rows + their norms
+    tile_bytes = tile_rows * (row_bytes + 4)  # rows + their norms
     fetched = {R: 0.0 for R in R_list}
     by_split = defaultdict(list)
     for b in range(len(split)):
@@ -140,11 +140,16 @@ def main():
     ap.add_argument("--config", default="d", choices=sorted(CONFIGS))
     ap.add_argument("--nq", type=int, default=0)
     ap.add_argument("--dump", default="")
+    ap.add_argument("--tile-rows", type=int, default=0,
+                    help="rows per scan tile (0: 64 where k_scan_v5 runs -- 16-bit rows at nq > 128 -- else 128)")
     args = ap.parse_args()
     path = Path(args.dump) if args.dump else Path(tempfile.mkdtemp()) / "scan_trace.bin"
     rows, d, dtype, nq, row_bytes, wall = run_trace(args.config, args.nq, path)
     tr = np.fromfile(path, dtype=np.uint64).reshape(-1, 4)
-    res = model(tr, rows, row_bytes, [20e-6, 40e-6, 80e-6])
+    v5 = os.environ.get("FX_SCAN_V5", "1") != "0" and dtype != "float32" and row_bytes in (512, 768, 1536) and nq > 128
+    tile_rows = args.tile_rows or (64 if v5 else 128)
+    res = model(tr, rows, row_bytes, [20e-6, 40e-6, 80e-6], tile_rows=tile_rows)
+    res["tile_rows"] = tile_rows
     alg = rows * row_bytes
     res["modelled_x_algorithmic"] = {k: round(v / alg, 2) for k, v in res["modelled_past_l2_bytes"].items()}
     res.update({"config": args.config, "rows": rows, "dim": d, "dtype": dtype, "nq": nq,

@@ -28,13 +28,31 @@
 namespace fx {
 namespace v5 {
 
+// A/B switches (make v5variant): ring slots, the MFMA row after which a
+// half-stage issues its corpus piece, the odd block's AGPR K-steps, the list
+// capacity of the 3-block instance
+#ifndef FX_V5_NS
+#define FX_V5_NS 5
+#endif
+#ifndef FX_V5_PIECE_M
+#define FX_V5_PIECE_M 2
+#endif
+#ifndef FX_V5_ODD_KA
+#define FX_V5_ODD_KA 14
+#endif
+#ifndef FX_V5_LC3
+#define FX_V5_LC3 64
+#endif
+
 constexpr int TR = 64;                 // corpus rows per tile
 constexpr int M = TR / 16;             // 16-row fragments per tile
-constexpr int NS = 5;                  // ring slots (NS - 1 stages in flight)
 constexpr int S_STAGE = TR * STAGE_B;  // 8 KiB: 64 rows x 128 B of K
 constexpr int PPS = S_STAGE / 1024 / 4;  // corpus pieces per wave per stage (2)
+// ring slots (NS - 1 stages in flight; the ring must not reach past the next tile)
+template <int KSTEPS>
+constexpr int ns_for() { return FX_V5_NS >= 6 && KSTEPS / 2 >= 5 ? 6 : 5; }
 
-template <int NB, int LC>
+template <int NB, int LC, int NS = 5>
 struct Lds {
     static constexpr int QW = 16 * NB;                             // queries per wave
     static constexpr int QT = 4 * QW;                              // per workgroup
@@ -254,7 +272,7 @@ __device__ __forceinline__ float min4_raw(float a, float b, float c, float d) {
 
 // K-steps of the odd query block whose B fragments sit in AGPRs (the rest in
 // VGPRs): 192 + 4 KA <= 256 AGPRs
-constexpr int ODD_KA = 14;
+constexpr int ODD_KA = FX_V5_ODD_KA;
 
 // MFMAs of one A fragment against NB query blocks (pairs through
 // AsmMmaV::mma2: B pinned in AGPRs; an odd last block through mma1)
@@ -275,7 +293,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v5(ScanParams p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     typedef typename AsmMmaV<DT>::A frag_t;
     typedef typename AsmMmaV<DT>::B bfrag_t;
-    typedef Lds<NB, LC> L;
+    constexpr int NS = ns_for<KSTEPS>();
+    typedef Lds<NB, LC, NS> L;
     constexpr int QW = L::QW, QT = L::QT, NSLOT = L::NSLOT, LST = L::LST;
     constexpr int SPT = KSTEPS / 2;  // stages per tile
     constexpr int RB = KSTEPS * 64;  // row stride in bytes
@@ -421,7 +440,9 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v5(ScanParams p) {
             const int tnext = t + (nxt ? 1 : 0);
             // VMEM ops younger than stage g+1's: stages g+2 .. g+NS-2 (PPS
             // corpus pieces each, + the norm piece with a tile's first stage)
-            constexpr int W = PPS * (NS - 3) + ((j + 2) % SPT == 0) + ((j + 3) % SPT == 0);
+            constexpr int W = PPS * (NS - 3) + ((j + 2) % SPT == 0) + ((j + 3) % SPT == 0) +
+                              (NS >= 6 && (j + 4) % SPT == 0);
+            static_assert(NS == 5 || NS == 6, "wait count written for 5 or 6 slots");
             asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(W) : "memory");
             __builtin_amdgcn_sched_barrier(0);
             constexpr int kq0 = 2 * j;
@@ -442,7 +463,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v5(ScanParams p) {
                     ds_rd128<m0 * NSLOT>(yin[m0], na);
                     ds_rd128<m1 * NSLOT>(yin[m1], na);
                 }
-                if constexpr (m == 2) piece(std::integral_constant<int, 0>{}, JP{}, NXT{}, c4, tnext);
+                if constexpr (m == FX_V5_PIECE_M) piece(std::integral_constant<int, 0>{}, JP{}, NXT{}, c4, tnext);
             });
             if constexpr (LAST) {
                 // epilogue operands of this tile: the queries' shared thresholds
@@ -463,7 +484,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v5(ScanParams p) {
                     ds_rd128<(2 * m) * 2048>(X[2 * m], rd_next);
                     ds_rd128<(2 * m + 1) * 2048>(X[2 * m + 1], rd_next);
                 }
-                if constexpr (m == 2) piece(std::integral_constant<int, 1>{}, JP{}, NXT{}, c4, tnext);
+                if constexpr (m == FX_V5_PIECE_M) piece(std::integral_constant<int, 1>{}, JP{}, NXT{}, c4, tnext);
                 if constexpr (m == 3 && jp == 0) piece(std::integral_constant<int, PPS>{}, JP{}, NXT{}, c4, tnext);
             });
             __builtin_amdgcn_sched_barrier(0);
@@ -625,7 +646,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v5(ScanParams p) {
 
 template <int DT, int METRIC, int KSTEPS, int NB, int LC, int ABL>
 static hipError_t launch_t(const ScanParams& p, hipStream_t s) {
-    constexpr int LDS_BYTES = Lds<NB, LC>::BYTES;
+    constexpr int LDS_BYTES = Lds<NB, LC, ns_for<KSTEPS>()>::BYTES;
     hipError_t e = g_graph_capture ? hipSuccess
                                    : hipFuncSetAttribute((const void*)k_scan_v5<DT, METRIC, KSTEPS, NB, LC, ABL>,
                                                          hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
@@ -637,15 +658,24 @@ static hipError_t launch_t(const ScanParams& p, hipStream_t s) {
 
 template <int DT, int METRIC>
 static hipError_t rows(const ScanParams& p, hipStream_t s) {
+#ifdef FX_V5_DEV  // kernel-development A/B builds: config (d)'s instance only
+    if constexpr (DT == BF16 && METRIC == L2)
+        if (p.row_bytes == 1536)
+            return p.nq_dev ? launch_t<DT, METRIC, 24, 3, FX_V5_LC3, RESCAN>(p, s)
+                            : launch_t<DT, METRIC, 24, 3, FX_V5_LC3, 0>(p, s);
+    return hipErrorInvalidValue;
+#else
     // the re-scan of uncertified queries (p.nq_dev set) runs the same code under its own name
     switch (p.row_bytes / 64) {
         case 8: return p.nq_dev ? launch_t<DT, METRIC, 8, 4, 48, RESCAN>(p, s) : launch_t<DT, METRIC, 8, 4, 48, 0>(p, s);
         case 12:
             return p.nq_dev ? launch_t<DT, METRIC, 12, 4, 48, RESCAN>(p, s) : launch_t<DT, METRIC, 12, 4, 48, 0>(p, s);
         case 24:
-            return p.nq_dev ? launch_t<DT, METRIC, 24, 3, 64, RESCAN>(p, s) : launch_t<DT, METRIC, 24, 3, 64, 0>(p, s);
+            return p.nq_dev ? launch_t<DT, METRIC, 24, 3, FX_V5_LC3, RESCAN>(p, s)
+                            : launch_t<DT, METRIC, 24, 3, FX_V5_LC3, 0>(p, s);
         default: return hipErrorInvalidValue;
     }
+#endif
 }
 
 }  // namespace v5

@@ -31,8 +31,8 @@ namespace v5 {
 // A/B switches (make v5variant): ring slots, the MFMA row after which a
 // half-stage issues its corpus piece, the odd block's AGPR K-steps, the list
 // capacity of the 3-block instance
-#ifndef FX_V5_NS
-#define FX_V5_NS 5
+#ifndef FX_V5_NS3
+#define FX_V5_NS3 6
 #endif
 #ifndef FX_V5_PIECE_M
 #define FX_V5_PIECE_M 2
@@ -41,16 +41,29 @@ namespace v5 {
 #define FX_V5_ODD_KA 14
 #endif
 #ifndef FX_V5_LC3
-#define FX_V5_LC3 64
+#define FX_V5_LC3 48
 #endif
 
 constexpr int TR = 64;                 // corpus rows per tile
 constexpr int M = TR / 16;             // 16-row fragments per tile
 constexpr int S_STAGE = TR * STAGE_B;  // 8 KiB: 64 rows x 128 B of K
 constexpr int PPS = S_STAGE / 1024 / 4;  // corpus pieces per wave per stage (2)
-// ring slots (NS - 1 stages in flight; the ring must not reach past the next tile)
-template <int KSTEPS>
-constexpr int ns_for() { return FX_V5_NS >= 6 && KSTEPS / 2 >= 5 ? 6 : 5; }
+// ring slots (NS - 1 stages in flight; the ring must not reach past the next
+// tile): the 3-block instance has the LDS for FX_V5_NS3 slots with 48-entry
+// lists (same box, profiles/r6/ab_v5_variants_*_r6k.txt: 6 slots (d) -1.2 %,
+// the N = 8 shard -0.5 % against 5 slots with 64-entry lists); the 4-block
+// instance's 256 lists leave room for 5
+template <int KSTEPS, int NB>
+constexpr int ns_for() { return NB == 3 && FX_V5_NS3 - 1 <= KSTEPS / 2 ? FX_V5_NS3 : 5; }
+// VMEM operations issued after stage g+1's at the wait of stage j (a tile's
+// stage): PPS corpus pieces per stage for stages g+2 .. g+NS-2, plus the norm
+// piece of every tile's first stage among them
+template <int NS, int SPT>
+constexpr int younger(int j) {
+    int w = PPS * (NS - 3);
+    for (int d = 2; d <= NS - 2; ++d) w += (j + d) % SPT == 0;
+    return w;
+}
 
 template <int NB, int LC, int NS = 5>
 struct Lds {
@@ -293,7 +306,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v5(ScanParams p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     typedef typename AsmMmaV<DT>::A frag_t;
     typedef typename AsmMmaV<DT>::B bfrag_t;
-    constexpr int NS = ns_for<KSTEPS>();
+    constexpr int NS = ns_for<KSTEPS, NB>();
     typedef Lds<NB, LC, NS> L;
     constexpr int QW = L::QW, QT = L::QT, NSLOT = L::NSLOT, LST = L::LST;
     constexpr int SPT = KSTEPS / 2;  // stages per tile
@@ -440,9 +453,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v5(ScanParams p) {
             const int tnext = t + (nxt ? 1 : 0);
             // VMEM ops younger than stage g+1's: stages g+2 .. g+NS-2 (PPS
             // corpus pieces each, + the norm piece with a tile's first stage)
-            constexpr int W = PPS * (NS - 3) + ((j + 2) % SPT == 0) + ((j + 3) % SPT == 0) +
-                              (NS >= 6 && (j + 4) % SPT == 0);
-            static_assert(NS == 5 || NS == 6, "wait count written for 5 or 6 slots");
+            constexpr int W = younger<NS, SPT>(j);
             asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"i"(W) : "memory");
             __builtin_amdgcn_sched_barrier(0);
             constexpr int kq0 = 2 * j;
@@ -646,7 +657,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v5(ScanParams p) {
 
 template <int DT, int METRIC, int KSTEPS, int NB, int LC, int ABL>
 static hipError_t launch_t(const ScanParams& p, hipStream_t s) {
-    constexpr int LDS_BYTES = Lds<NB, LC, ns_for<KSTEPS>()>::BYTES;
+    constexpr int LDS_BYTES = Lds<NB, LC, ns_for<KSTEPS, NB>()>::BYTES;
     hipError_t e = g_graph_capture ? hipSuccess
                                    : hipFuncSetAttribute((const void*)k_scan_v5<DT, METRIC, KSTEPS, NB, LC, ABL>,
                                                          hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);

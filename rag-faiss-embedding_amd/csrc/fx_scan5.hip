@@ -43,6 +43,12 @@ namespace v5 {
 #ifndef FX_V5_LC3
 #define FX_V5_LC3 48
 #endif
+#ifndef FX_V5_NS4
+#define FX_V5_NS4 5
+#endif
+#ifndef FX_V5_LC4
+#define FX_V5_LC4 48
+#endif
 
 constexpr int TR = 64;                 // corpus rows per tile
 constexpr int M = TR / 16;             // 16-row fragments per tile
@@ -54,7 +60,11 @@ constexpr int PPS = S_STAGE / 1024 / 4;  // corpus pieces per wave per stage (2)
 // the N = 8 shard -0.5 % against 5 slots with 64-entry lists); the 4-block
 // instance's 256 lists leave room for 5
 template <int KSTEPS, int NB>
-constexpr int ns_for() { return NB == 3 && FX_V5_NS3 - 1 <= KSTEPS / 2 ? FX_V5_NS3 : 5; }
+constexpr int ns_for() {
+    return NB == 3 && FX_V5_NS3 - 1 <= KSTEPS / 2   ? FX_V5_NS3
+           : NB == 4 && FX_V5_NS4 - 1 <= KSTEPS / 2 ? FX_V5_NS4
+                                                   : 5;
+}
 // VMEM operations issued after stage g+1's at the wait of stage j (a tile's
 // stage): PPS corpus pieces per stage for stages g+2 .. g+NS-2, plus the norm
 // piece of every tile's first stage among them
@@ -669,18 +679,25 @@ static hipError_t launch_t(const ScanParams& p, hipStream_t s) {
 
 template <int DT, int METRIC>
 static hipError_t rows(const ScanParams& p, hipStream_t s) {
-#ifdef FX_V5_DEV  // kernel-development A/B builds: config (d)'s instance only
+#ifdef FX_V5_DEV  // kernel-development A/B builds: configs (d) and (e)'s instances only
     if constexpr (DT == BF16 && METRIC == L2)
         if (p.row_bytes == 1536)
             return p.nq_dev ? launch_t<DT, METRIC, 24, 3, FX_V5_LC3, RESCAN>(p, s)
                             : launch_t<DT, METRIC, 24, 3, FX_V5_LC3, 0>(p, s);
+    if constexpr (DT == F16 && METRIC == L2)
+        if (p.row_bytes == 768)
+            return p.nq_dev ? launch_t<DT, METRIC, 12, 4, FX_V5_LC4, RESCAN>(p, s)
+                            : launch_t<DT, METRIC, 12, 4, FX_V5_LC4, 0>(p, s);
     return hipErrorInvalidValue;
 #else
     // the re-scan of uncertified queries (p.nq_dev set) runs the same code under its own name
     switch (p.row_bytes / 64) {
-        case 8: return p.nq_dev ? launch_t<DT, METRIC, 8, 4, 48, RESCAN>(p, s) : launch_t<DT, METRIC, 8, 4, 48, 0>(p, s);
+        case 8:
+            return p.nq_dev ? launch_t<DT, METRIC, 8, 4, FX_V5_LC4, RESCAN>(p, s)
+                            : launch_t<DT, METRIC, 8, 4, FX_V5_LC4, 0>(p, s);
         case 12:
-            return p.nq_dev ? launch_t<DT, METRIC, 12, 4, 48, RESCAN>(p, s) : launch_t<DT, METRIC, 12, 4, 48, 0>(p, s);
+            return p.nq_dev ? launch_t<DT, METRIC, 12, 4, FX_V5_LC4, RESCAN>(p, s)
+                            : launch_t<DT, METRIC, 12, 4, FX_V5_LC4, 0>(p, s);
         case 24:
             return p.nq_dev ? launch_t<DT, METRIC, 24, 3, FX_V5_LC3, RESCAN>(p, s)
                             : launch_t<DT, METRIC, 24, 3, FX_V5_LC3, 0>(p, s);

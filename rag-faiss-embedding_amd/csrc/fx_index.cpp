@@ -117,7 +117,8 @@ struct Options {
                              // SMALL_NQ instance); 0: the ordinary instance
     int refine_waves = REFINE_WG_WAVES;  // FX_REFINE_WAVES: waves of k_refine_wg's workgroup (4, 8, 16)
     int scan_v5 = 1;         // FX_SCAN_V5: 16-bit rows of 512 / 768 / 1,536 B scan with k_scan_v5 (64-row
-                             // tiles, 256 / 192 queries per workgroup; fx_scan5.hip); 0: k_scan_v4
+                             // tiles, 256 / 192 queries per workgroup; fx_scan5.hip) where it adds no
+                             // padding work; 2: wherever it has the shape (tests); 0: k_scan_v4
     int host_spin = 1;       // FX_HOST_SPIN: a host-output search waits for its results by polling the
                              // stream (1) instead of a blocking hipStreamSynchronize (0)
 #ifdef FX_DIAG
@@ -193,7 +194,7 @@ struct Options {
             {"tight_at", &tight_at, -1, CAP, nullptr, 0},
             {"cold_bound", &cold_bound, -1, 1, nullptr, 0},
             {"host_spin", &host_spin, 0, 1, nullptr, 0},
-            {"scan_v5", &scan_v5, 0, 1, nullptr, 0},
+            {"scan_v5", &scan_v5, 0, 2, nullptr, 0},
             {"refine_waves", &refine_waves, 4, 16, kWaves, 3},
             {"small_scan", &small_scan, 0, 1, nullptr, 0},
 #ifdef FX_DIAG
@@ -394,7 +395,7 @@ void plan_scan(const FxIndex* h, int64_t nq, int k, ScanParams& p) {
     // calls keep k_scan_v4's 128-query tile)
     const int v5qt = h->opt.scan_v5 != 0 && !(h->opt.scan_dbg & 32) ? scan_v5_qt(sdt, h->row_bytes) : 0;
     const int64_t slots4 = (nq + TILE_Q - 1) / TILE_Q * TILE_Q;
-    const bool v5 = v5qt > 0 && (nq + v5qt - 1) / v5qt * v5qt * 20 <= slots4 * 21;
+    const bool v5 = v5qt > 0 && (h->opt.scan_v5 == 2 || (nq + v5qt - 1) / v5qt * v5qt * 20 <= slots4 * 21);
     p.qt = v5 ? v5qt : TILE_Q;
     p.small_ok = h->opt.small_scan != 0 && !(h->opt.scan_dbg & 32) ? 1 : 0;
     p.tr = v5 ? V5_TR : TILE_R;

@@ -109,14 +109,18 @@ struct ScanLds {
 //           undo it, conflict-free for both K halves.
 constexpr int RESCAN = 4096;  // ABL bit naming the re-scan's instance (no code change)
 // ABL bit of the small-batch instance (nq <= 16: only wave 0's first query
-// block can hold a live query): the other blocks' MFMAs and query loads are
-// skipped, so the one-query call's DMA is no longer paced by 127 padding
-// queries' MFMAs (results valid: the skipped blocks have no live query, their
-// thresholds are -inf and they never push)
+// block can hold a live query): waves 1-3 skip their MFMAs and query loads
+// (results valid: they hold no live query, their thresholds are -inf and they
+// never push)
 constexpr int SMALL_NQ = 16384;
 
-// a pair of query blocks' MFMAs of one A fragment; SMALL: only block 0, and
-// only on wave 0 (wave-uniform branch)
+// a pair of query blocks' MFMAs of one A fragment; SMALL: only on wave 0
+// (wave-uniform branch).  Wave 0 keeps BOTH MFMAs of the pair: an operand
+// fragment is overwritten by its next ds_read >= 8 MFMAs after its last MFMA
+// reader, and with one MFMA per fragment that distance halves -- a first
+// version that skipped block 1 on wave 0 returned wrong keys for bf16 rows
+// (tests/test_scan_v5.py, the v4 arm at nq = 1): the MFMAs read their A
+// operand later than they issue
 template <int DT, int INIT, bool SMALL>
 __device__ __forceinline__ void mma_pair(f32x4& c0, f32x4& c1, const typename AsmMmaV<DT>::A& a,
                                          const typename AsmMmaV<DT>::B& b0, const typename AsmMmaV<DT>::B& b1,
@@ -124,9 +128,7 @@ __device__ __forceinline__ void mma_pair(f32x4& c0, f32x4& c1, const typename As
     if constexpr (!SMALL) {
         AsmMmaV<DT>::template mma2<INIT>(c0, c1, a, b0, b1, ci);
     } else {
-        (void)c1;
-        (void)b1;
-        if (w0) mma1<DT, INIT, true>(c0, a, b0, ci);
+        if (w0) AsmMmaV<DT>::template mma2<INIT>(c0, c1, a, b0, b1, ci);
     }
 }
 

@@ -107,7 +107,10 @@ int fx_index_set_stream(FxIndex* index, void* stream);
  * entries and holds at least this many gets its threshold re-bounded between
  * compactions), "cold_bound" -1/0/1 (an empty list's first record tile bounds its
  * threshold from the per-lane group minima; -1, the default: on for corpus
- * splits of <= 256 tiles).  None changes results, only
+ * splits of <= 256 tiles), "scan_v5" 0/1/2 (default 1: the 64-row-tile scan
+ * for 16-bit rows of 512 / 768 / 1536 B where it adds no padding work; 2
+ * wherever it has the shape), "refine_waves" 4/8/16,
+ * "host_spin" 0/1.  None changes results, only
  * speed.  Unknown name or out-of-range value: FX_E_ARG.  (The diagnostic
  * build libfx_index_diag.so adds test hooks -- "force_fallback",
  * "scan_dbg" -- that the product library does not have.) */

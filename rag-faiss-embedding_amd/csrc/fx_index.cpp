@@ -113,8 +113,6 @@ struct Options {
                              // at nq = 256 (short splits), +0.5-0.9 % on the long splits of (d) and the
                              // N = 8 shard (r5h, r5i, r5k)
     int graph_verbose = 0;   // FX_SEARCH_GRAPH_VERBOSE
-    int small_scan = 1;      // FX_SMALL_SCAN: nq <= 16 scans skip the padding query blocks' MFMAs (k_scan_v4
-                             // SMALL_NQ instance); 0: the ordinary instance
     int refine_waves = REFINE_WG_WAVES;  // FX_REFINE_WAVES: waves of k_refine_wg's workgroup (4, 8, 16)
     int scan_v5 = 1;         // FX_SCAN_V5: 16-bit rows of 512 / 768 / 1,536 B scan with k_scan_v5 (64-row
                              // tiles, 256 / 192 queries per workgroup; fx_scan5.hip) where it adds no
@@ -154,7 +152,6 @@ struct Options {
         num("FX_HOST_SPIN", host_spin);
         num("FX_SCAN_V5", scan_v5);
         num("FX_REFINE_WAVES", refine_waves);
-        num("FX_SMALL_SCAN", small_scan);
         if (refine_waves != 4 && refine_waves != 8 && refine_waves != 16) refine_waves = REFINE_WG_WAVES;
         (void)str;
 #ifdef FX_DIAG
@@ -196,7 +193,6 @@ struct Options {
             {"host_spin", &host_spin, 0, 1, nullptr, 0},
             {"scan_v5", &scan_v5, 0, 2, nullptr, 0},
             {"refine_waves", &refine_waves, 4, 16, kWaves, 3},
-            {"small_scan", &small_scan, 0, 1, nullptr, 0},
 #ifdef FX_DIAG
             {"force_fallback", &force_fallback, 0, 2, nullptr, 0},
             {"scan_dbg", &scan_dbg, 0, 1 << 20, nullptr, 0},
@@ -397,7 +393,6 @@ void plan_scan(const FxIndex* h, int64_t nq, int k, ScanParams& p) {
     const int64_t slots4 = (nq + TILE_Q - 1) / TILE_Q * TILE_Q;
     const bool v5 = v5qt > 0 && (h->opt.scan_v5 == 2 || (nq + v5qt - 1) / v5qt * v5qt * 20 <= slots4 * 21);
     p.qt = v5 ? v5qt : TILE_Q;
-    p.small_ok = h->opt.small_scan != 0 && !(h->opt.scan_dbg & 32) ? 1 : 0;
     p.tr = v5 ? V5_TR : TILE_R;
     p.n_qtiles = (int)((nq + p.qt - 1) / p.qt);
     p.n_ctiles = (int)((h->ntotal + p.tr - 1) / p.tr);
@@ -1071,7 +1066,7 @@ std::vector<uint64_t> graph_key(const FxIndex* h, int64_t nq, int q_dtype, int k
             (uint64_t)o.force_fallback, (uint64_t)o.place, (uint64_t)o.sx, (uint64_t)o.reduce_cand,
             (uint64_t)o.pub, (uint64_t)o.prune_rank, (uint64_t)o.compact_at, (uint64_t)o.union_w,
             (uint64_t)o.union_defer, (uint64_t)(int64_t)o.union_inplace, (uint64_t)(int64_t)o.tight_at, (uint64_t)o.cold_bound,
-            (uint64_t)o.reduce_cand, (uint64_t)o.scan_v5, (uint64_t)o.refine_waves, (uint64_t)o.small_scan,
+            (uint64_t)o.reduce_cand, (uint64_t)o.scan_v5, (uint64_t)o.refine_waves,
             (uint64_t)(uintptr_t)h->codes, (uint64_t)(uintptr_t)h->norms, (uint64_t)(uintptr_t)h->split.p,
             (uint64_t)(uintptr_t)h->cnorms.p, (uint64_t)(uintptr_t)h->centre.p, (uint64_t)(uintptr_t)h->qshift.p,
             (uint64_t)(uintptr_t)h->qin.p, (uint64_t)(uintptr_t)h->qf32.p, (uint64_t)(uintptr_t)h->qop.p,

@@ -84,7 +84,6 @@ struct ScanParams {
     int qt;                     // queries per scan tile (the candidate layout's [qtile][split][qt][KP]):
                                 // TILE_Q (k_scan_v4 / k_scan_topk) or 256 (k_scan_v5)
     int tr;                     // corpus rows per scan tile: TILE_R, or 64 (k_scan_v5)
-    int small_ok;               // 1: nq <= 16 may take k_scan_v4's small-batch instance (option small_scan)
 };
 
 // queries are zero-padded to a multiple of QPAD (the scan's query tile)

@@ -108,30 +108,6 @@ struct ScanLds {
 //           address (LDS-DMA writes lane-linearly), and the fragment reads
 //           undo it, conflict-free for both K halves.
 constexpr int RESCAN = 4096;  // ABL bit naming the re-scan's instance (no code change)
-// ABL bit of the small-batch instance (nq <= 16: only wave 0's first query
-// block can hold a live query): waves 1-3 skip their MFMAs and query loads
-// (results valid: they hold no live query, their thresholds are -inf and they
-// never push)
-constexpr int SMALL_NQ = 16384;
-
-// a pair of query blocks' MFMAs of one A fragment; SMALL: only on wave 0
-// (wave-uniform branch).  Wave 0 keeps BOTH MFMAs of the pair: an operand
-// fragment is overwritten by its next ds_read >= 8 MFMAs after its last MFMA
-// reader, and with one MFMA per fragment that distance halves -- a first
-// version that skipped block 1 on wave 0 returned wrong keys for bf16 rows
-// (tests/test_scan_v5.py, the v4 arm at nq = 1): the MFMAs read their A
-// operand later than they issue
-template <int DT, int INIT, bool SMALL>
-__device__ __forceinline__ void mma_pair(f32x4& c0, f32x4& c1, const typename AsmMmaV<DT>::A& a,
-                                         const typename AsmMmaV<DT>::B& b0, const typename AsmMmaV<DT>::B& b1,
-                                         const f32x4& ci, bool w0) {
-    if constexpr (!SMALL) {
-        AsmMmaV<DT>::template mma2<INIT>(c0, c1, a, b0, b1, ci);
-    } else {
-        if (w0) AsmMmaV<DT>::template mma2<INIT>(c0, c1, a, b0, b1, ci);
-    }
-}
-
 template <int DT, int METRIC, int KSTEPS, int ABL = 0, int LN = 0>
 __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -145,11 +121,9 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
     constexpr int RB = KSTEPS * 64;  // row stride in bytes
     constexpr int64_t TILE_BYTES = (int64_t)TILE_R * RB;
     static_assert(SPT >= NS - 1, "prefetch distance must stay within the next tile");
-    constexpr bool SMALL = (ABL & SMALL_NQ) != 0;
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const bool w0 = wave == 0;
     int qtile, split;
     map_block(blockIdx.x, p, qtile, split);
     // the live query count (the re-scan of uncertified queries learns it on the device)
@@ -182,7 +156,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
         for (int ks = 0; ks < KSTEPS; ++ks)
 #pragma unroll
             for (int n = 0; n < N; ++n)
-                b[ks][n] = SMALL && (!w0 || n != 0) ? bfrag_t{} : *(const bfrag_t*)(qb + n * 16 * RB + ks * 64);
+                b[ks][n] = *(const bfrag_t*)(qb + n * 16 * RB + ks * 64);
 #pragma unroll
         for (int ks = 0; ks < KSTEPS; ++ks)
 #pragma unroll
@@ -353,7 +327,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
                 constexpr int m = decltype(MM)::value;
                 constexpr int INIT = j == 0 ? (METRIC == L2 ? 1 : 2) : 0;
                 if constexpr (!(ABL & 4))
-                    mma_pair<DT, INIT, SMALL>(acc[m][0], acc[m][1], X[m], b[kq0][0], b[kq0][1], yin[m], w0);
+                    AsmMmaV<DT>::template mma2<INIT>(acc[m][0], acc[m][1], X[m], b[kq0][0], b[kq0][1], yin[m]);
                 // half 1 of this stage: two reads per pair over the first four
                 // pairs, so the mid-stage wait finds them landed
                 if constexpr (m < M / 2 && !(EB && j == 0)) {  // EB: stage 0's Y read at the tile end
@@ -381,8 +355,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
             if constexpr (HI) {  // hi * x_lo (>= 14 MFMAs after each accumulator's previous write)
                 static_for<M>([&](auto MM) {
                     constexpr int m = decltype(MM)::value;
-                    mma_pair<DT, 0, SMALL>(acc[m][0], acc[m][1], X[m], b[2 * j + KH][0], b[2 * j + KH][1], yin[m],
-                                           w0);
+                    AsmMmaV<DT>::template mma2<0>(acc[m][0], acc[m][1], X[m], b[2 * j + KH][0], b[2 * j + KH][1],
+                                                  yin[m]);
                 });
             }
             if constexpr (LAST) {
@@ -409,7 +383,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
             static_for<M>([&](auto MM) {
                 constexpr int m = decltype(MM)::value;
                 if constexpr (!(ABL & 4))
-                    mma_pair<DT, 0, SMALL>(acc[m][0], acc[m][1], Y[m], b[kq0 + 1][0], b[kq0 + 1][1], yin[m], w0);
+                    AsmMmaV<DT>::template mma2<0>(acc[m][0], acc[m][1], Y[m], b[kq0 + 1][0], b[kq0 + 1][1], yin[m]);
                 // half 0 of stage g+1: two reads per pair over the first four
                 // pairs (X[2m+1]'s last reader is >= 8 MFMAs back)
                 if constexpr (m < M / 2) {
@@ -425,8 +399,8 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
             if constexpr (HI) {
                 static_for<M>([&](auto MM) {
                     constexpr int m = decltype(MM)::value;
-                    mma_pair<DT, 0, SMALL>(acc[m][0], acc[m][1], Y[m], b[2 * j + 1 + KH][0], b[2 * j + 1 + KH][1],
-                                           yin[m], w0);
+                    AsmMmaV<DT>::template mma2<0>(acc[m][0], acc[m][1], Y[m], b[2 * j + 1 + KH][0],
+                                                  b[2 * j + 1 + KH][1], yin[m]);
                 });
             }
             __builtin_amdgcn_sched_barrier(0);
@@ -759,24 +733,14 @@ static hipError_t scan_rows(const ScanParams& p, hipStream_t s, bool* handled) {
     *handled = false;
     return hipSuccess;
 #else
-    // small batches (nq <= 16, one live query block) of the common row widths
-    // take the SMALL_NQ instance (L2, 16-bit and split-fp32 scans)
-    constexpr bool HAS_SMALL = METRIC == L2 && DT != F32;
-    const bool small = HAS_SMALL && !p.nq_dev && p.nq <= 16 && p.small_ok;
     switch (p.row_bytes / 64) {
         // the re-scan of uncertified queries (p.nq_dev set) runs the same code
         // under its own kernel name (ABL bit RESCAN changes nothing else), so
         // profiles keep the main scan's launches apart from it
         case 8: return p.nq_dev ? scan_v4_t<DT, METRIC, 8, RESCAN>(p, s) : scan_v4_t<DT, METRIC, 8>(p, s);
-        case 12:
-            if constexpr (HAS_SMALL)
-                if (small) return scan_v4_t<DT, METRIC, 12, SMALL_NQ>(p, s);
-            return p.nq_dev ? scan_v4_t<DT, METRIC, 12, RESCAN>(p, s) : scan_v4_t<DT, METRIC, 12>(p, s);
+        case 12: return p.nq_dev ? scan_v4_t<DT, METRIC, 12, RESCAN>(p, s) : scan_v4_t<DT, METRIC, 12>(p, s);
         case 16: return p.nq_dev ? scan_v4_t<DT, METRIC, 16, RESCAN>(p, s) : scan_v4_t<DT, METRIC, 16>(p, s);
-        case 24:
-            if constexpr (HAS_SMALL)
-                if (small) return scan_v4_t<DT, METRIC, 24, SMALL_NQ>(p, s);
-            return p.nq_dev ? scan_v4_t<DT, METRIC, 24, RESCAN>(p, s) : scan_v4_t<DT, METRIC, 24>(p, s);
+        case 24: return p.nq_dev ? scan_v4_t<DT, METRIC, 24, RESCAN>(p, s) : scan_v4_t<DT, METRIC, 24>(p, s);
         default: *handled = false; return hipSuccess;
     }
 #endif

@@ -71,3 +71,41 @@ def test_scan_kernels_use_no_scratch(asm_files, unit):
     assert sizes, "no k_scan_v4 / k_scan_v5 kernel metadata found"
     bad = [(n, int(v)) for n, v in sizes if int(v) != 0]
     assert not bad, f"scan kernels with scratch: {bad}"
+
+
+def _kernel_bodies(text, pattern):
+    """(name, body) of each kernel whose symbol matches `pattern` in a .s file."""
+    import re
+    out = []
+    for m in re.finditer(r"^(" + pattern + r"):", text, re.M):
+        end = text.find(".Lfunc_end", m.end())
+        out.append((m.group(1), text[m.end():end]))
+    return out
+
+
+@pytest.mark.parametrize("unit", UNITS)
+def test_scan_query_fragments_stay_in_place(asm_files, unit):
+    """The queries' B fragments are settled in AGPRs once per workgroup and
+    read by inline-asm MFMAs the compiler cannot see in flight: an AGPR move
+    or a re-write between them can land while an MFMA still reads the
+    register.  A small-batch instance whose wave-uniform branch made the
+    allocator shuffle them (1,161 v_accvgpr_mov) returned wrong neighbours
+    (DESIGN.md 3.1b), so no scan instance may move AGPRs, and AGPR writes stay
+    the handful outside the stage loop."""
+    text = asm_files[unit].read_text()
+    bodies = _kernel_bodies(text, r"_ZN2fx\w*?k_scan_v[45]\w+")
+    assert bodies, "no k_scan_v4 / k_scan_v5 kernels found"
+    bad = []
+    for name, body in bodies:
+        mov = body.count("v_accvgpr_mov")
+        wr = body.count("v_accvgpr_write")
+        if mov or wr > 16:
+            bad.append((name, mov, wr))
+    assert not bad, f"scan kernels moving AGPRs (name, moves, writes): {bad}"
+
+
+def test_fragment_check_flags_moves():
+    body = "\tv_mfma_f32_16x16x32_bf16 v[0:3], v[4:7], a[0:3], v[0:3]\n\tv_accvgpr_mov_b32 a0, a4\n"
+    text = "_ZN2fx9k_scan_v4ILi1EEEvNS_10ScanParamsE:\n" + body + ".Lfunc_end0:\n"
+    (name, b), = _kernel_bodies(text, r"_ZN2fx\w*?k_scan_v[45]\w+")
+    assert b.count("v_accvgpr_mov") == 1

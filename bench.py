@@ -511,9 +511,11 @@ def main():
     variant = os.environ.get("FX_F32_SPLIT", "1") == "0"
     roof["traffic"], roof["traffic_source"] = (None, None) if variant else \
         read_pmc_traffic(args.config, n_local, nq, args.data)
-    roof["kernel"] = "k_scan_v4" + \
+    plan = ix.last_scan_plan()  # the timed searches' scan kernel (k_scan_v5: 64-row tiles)
+    roof["kernel"] = ("k_scan_v5" if plan["tile_rows"] == 64 else "k_scan_v4") + \
         (" F32S (fp32 as 3 bf16 MFMA products)" if split else "") + \
         " (fused MFMA distance GEMM + top-k select)"
+    roof["scan_plan"] = plan
     roof["kernel_ms_avg"] = round(scan_avg_ms, 4)
     roof["launches"] = launches
     roof["merge_refine_ms_avg"] = round(merge_ms / max(launches, 1), 4)

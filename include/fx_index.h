@@ -165,6 +165,12 @@ int fx_index_last_exact_fallbacks(FxIndex* index, int64_t* out);
  * (this call synchronises the index stream). */
 int fx_index_last_dropped_candidates(FxIndex* index, int64_t* out);
 
+/* The scan plan of the last search (no faiss counterpart: which scan kernel
+ * ran, for benchmarks and profiles): tile_rows 128 = k_scan_v4, 64 =
+ * k_scan_v5; query_tile = queries per workgroup; splits = corpus splits per
+ * query tile.  All 0 before the first search. */
+int fx_index_last_scan_plan(FxIndex* index, int* tile_rows, int* query_tile, int* splits);
+
 /* IndexFlatL2 reset (faiss_store.py:124-128). Keeps the HBM allocation. */
 int fx_index_reset(FxIndex* index);
 

@@ -55,6 +55,7 @@ SIGNATURES = {
     "fx_index_add": (_i, [_vp, _i64, _vp, _i, _i]),
     "fx_index_search": (_i, [_vp, _i64, _vp, _i, _i, _i, _vp, _vp, _i]),
     "fx_index_last_fallbacks": (_i, [_vp, ctypes.POINTER(_i64)]),
+    "fx_index_last_scan_plan": (_i, [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i), ctypes.POINTER(_i)]),
     "fx_index_last_exact_fallbacks": (_i, [_vp, ctypes.POINTER(_i64)]),
     "fx_index_last_dropped_candidates": (_i, [_vp, ctypes.POINTER(_i64)]),
     "fx_index_reset": (_i, [_vp]),

@@ -117,6 +117,8 @@ struct Options {
     int scan_v5 = 1;         // FX_SCAN_V5: 16-bit rows of 512 / 768 / 1,536 B scan with k_scan_v5 (64-row
                              // tiles, 256 / 192 queries per workgroup; fx_scan5.hip) where it adds no
                              // padding work; 2: wherever it has the shape (tests); 0: k_scan_v4
+    int convoy = 1;          // FX_CONVOY: k_scan_v5 blocks start where the other blocks of their split
+                             // are (ScanParams.conv); 0: at the split's first tile
     int host_spin = 1;       // FX_HOST_SPIN: a host-output search waits for its results by polling the
                              // stream (1) instead of a blocking hipStreamSynchronize (0)
 #ifdef FX_DIAG
@@ -151,6 +153,7 @@ struct Options {
         num("FX_SEARCH_GRAPH_VERBOSE", graph_verbose);
         num("FX_HOST_SPIN", host_spin);
         num("FX_SCAN_V5", scan_v5);
+        num("FX_CONVOY", convoy);
         num("FX_REFINE_WAVES", refine_waves);
         if (refine_waves != 4 && refine_waves != 8 && refine_waves != 16) refine_waves = REFINE_WG_WAVES;
         (void)str;
@@ -192,6 +195,7 @@ struct Options {
             {"cold_bound", &cold_bound, -1, 1, nullptr, 0},
             {"host_spin", &host_spin, 0, 1, nullptr, 0},
             {"scan_v5", &scan_v5, 0, 2, nullptr, 0},
+            {"convoy", &convoy, 0, 1, nullptr, 0},
             {"refine_waves", &refine_waves, 4, 16, kWaves, 3},
 #ifdef FX_DIAG
             {"force_fallback", &force_fallback, 0, 2, nullptr, 0},
@@ -311,6 +315,8 @@ struct FxIndex {
     // (a corrupted candidate list; 0 unless something is broken)
     int64_t last_dropped = 0;
     int* dev_drop = nullptr;  // its device word, zeroed at the start of every search
+    DevBuf conv;  // k_scan_v5 convoy words (CONV_MAX; zeroed once, then only hints)
+    int last_plan[3] = {0, 0, 0};  // the last search's scan plan: tile rows (128 k_scan_v4, 64 k_scan_v5), qt, splits
     // profiling
     bool profile = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_scan, ev_merge;
@@ -630,6 +636,9 @@ hipError_t plan_search(FxIndex* h, int64_t nq, const void* qdev, int q_dtype, in
     P.scan_dt = h->img_kind == IMG_F32S ? (int)F32S : h->dtype;
     ScanParams& sp = P.sp;
     plan_scan(h, nq, k, sp);
+    h->last_plan[0] = sp.tr;
+    h->last_plan[1] = sp.qt;
+    h->last_plan[2] = sp.splits;
     P.nq_pad = round_up(nq, std::max<int64_t>(QPAD, sp.qt));  // whole scan tiles of (zero) queries
     const bool img = h->img_kind != IMG_NONE;
     if ((e = h->qf32.ensure((size_t)P.nq_pad * h->kdim * 4)) != hipSuccess) return e;
@@ -667,6 +676,14 @@ hipError_t plan_search(FxIndex* h, int64_t nq, const void* qdev, int q_dtype, in
     sp.dbg = h->opt.scan_dbg;
     if ((e = h->gtau.ensure((size_t)P.nq_pad * 4)) != hipSuccess) return e;
     sp.gtau = (unsigned*)h->gtau.p;
+    sp.conv = nullptr;
+    if (sp.tr == V5_TR && h->opt.convoy != 0 && sp.splits <= CONV_MAX) {
+        if (!h->conv.p) {
+            if ((e = h->conv.ensure((size_t)CONV_MAX * 4)) != hipSuccess) return e;
+            if ((e = hipMemsetAsync(h->conv.p, 0, (size_t)CONV_MAX * 4, h->stream())) != hipSuccess) return e;
+        }
+        sp.conv = (unsigned*)h->conv.p;
+    }
     // k_scan_v4's published per-split lists (the union threshold, see
     // compact_wave): slow-path tiles 25.7 -> 16.5 %, config (d) -3 %
     if (sp.share && sp.splits > 1 && h->opt.pub != 0) {
@@ -1066,14 +1083,14 @@ std::vector<uint64_t> graph_key(const FxIndex* h, int64_t nq, int q_dtype, int k
             (uint64_t)o.force_fallback, (uint64_t)o.place, (uint64_t)o.sx, (uint64_t)o.reduce_cand,
             (uint64_t)o.pub, (uint64_t)o.prune_rank, (uint64_t)o.compact_at, (uint64_t)o.union_w,
             (uint64_t)o.union_defer, (uint64_t)(int64_t)o.union_inplace, (uint64_t)(int64_t)o.tight_at, (uint64_t)o.cold_bound,
-            (uint64_t)o.reduce_cand, (uint64_t)o.scan_v5, (uint64_t)o.refine_waves,
+            (uint64_t)o.reduce_cand, (uint64_t)o.scan_v5, (uint64_t)o.refine_waves, (uint64_t)o.convoy,
             (uint64_t)(uintptr_t)h->codes, (uint64_t)(uintptr_t)h->norms, (uint64_t)(uintptr_t)h->split.p,
             (uint64_t)(uintptr_t)h->cnorms.p, (uint64_t)(uintptr_t)h->centre.p, (uint64_t)(uintptr_t)h->qshift.p,
             (uint64_t)(uintptr_t)h->qin.p, (uint64_t)(uintptr_t)h->qf32.p, (uint64_t)(uintptr_t)h->qop.p,
             (uint64_t)(uintptr_t)h->qeps.p, (uint64_t)(uintptr_t)h->qrho.p, (uint64_t)(uintptr_t)h->gtau.p,
             (uint64_t)(uintptr_t)h->pub.p, (uint64_t)(uintptr_t)h->cand_d.p, (uint64_t)(uintptr_t)h->cand_i.p,
             (uint64_t)(uintptr_t)h->cand2_d.p, (uint64_t)(uintptr_t)h->cand2_i.p,
-            (uint64_t)(uintptr_t)h->hout.p,
+            (uint64_t)(uintptr_t)h->hout.p, (uint64_t)(uintptr_t)h->conv.p,
             (uint64_t)(uintptr_t)h->flag.p, (uint64_t)(uintptr_t)h->fbc_d.p, (uint64_t)(uintptr_t)h->fbc_i.p,
             (uint64_t)(uintptr_t)h->rq_f32.p, (uint64_t)(uintptr_t)h->rq_op.p, (uint64_t)(uintptr_t)h->rq_eps.p,
             (uint64_t)(uintptr_t)h->rq_rho.p, (uint64_t)(uintptr_t)h->rq_shift.p, (uint64_t)(uintptr_t)h->rq_gtau.p,
@@ -1230,7 +1247,7 @@ void fx_index_free(FxIndex* h) {
                           &h->fbc_d, &h->fbc_i, &h->stage, &h->gtau, &h->trace, &h->dbgbuf, &h->split, &h->cnorms,
                           &h->centre, &h->mu_part, &h->qshift, &h->qrho, &h->stamps, &h->pub, &h->cand2_d,
                           &h->cand2_i, &h->rq_f32, &h->rq_op, &h->rq_eps, &h->rq_rho, &h->rq_shift, &h->rq_gtau,
-                          &h->rq_cand_d, &h->rq_cand_i, &h->rq_flag, &h->hk_ws, &h->hout})
+                          &h->rq_cand_d, &h->rq_cand_i, &h->rq_flag, &h->hk_ws, &h->hout, &h->conv})
             b->release();
         graph_release(h);
         if (h->ghq) (void)hipHostFree(h->ghq);
@@ -1421,6 +1438,15 @@ int fx_index_last_fallbacks(FxIndex* h, int64_t* out) {
     const int rc = read_counts(h);
     if (rc != FX_OK) return rc;
     *out = h->last_fallbacks;
+    return FX_OK;
+}
+
+int fx_index_last_scan_plan(FxIndex* h, int* tile_rows, int* query_tile, int* splits) {
+    if (!h || !tile_rows || !query_tile || !splits) return set_err(FX_E_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(h->mu);
+    *tile_rows = h->last_plan[0];
+    *query_tile = h->last_plan[1];
+    *splits = h->last_plan[2];
     return FX_OK;
 }
 

@@ -377,13 +377,31 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v5(ScanParams p) {
     const uint32_t lds_base = lds_off(smem);
     const uint32_t m0w = lds_base + L::RING_OFF + wave * (S_STAGE / 4);
     const uint32_t nslot_w = lds_base + L::NORM_OFF + wave * NSLOT;
-    const char* cb_cur = sgpr_ptr(p.codes + (int64_t)ct0 * TILE_BYTES);
-    const char* cb_nxt = sgpr_ptr(ntiles > 1 ? cb_cur + TILE_BYTES : cb_cur);
+    // convoy start: the split-relative tile another block of this split
+    // published last (any value is a valid start: the block scans its
+    // ntiles tiles circularly from it; results do not depend on the order).
+    // Read ONCE per block and passed to the other waves through LDS (the list
+    // area, not yet in use): every wave DMAs its own pieces of each shared
+    // stage, so waves that each read the word -- and saw a store land between
+    // their reads -- would fill one stage from two tiles (caught by
+    // test_v5_clustered_certifies: rows of one split missing)
+    int rel = 0;
+    if (p.conv && ntiles > 1) {
+        unsigned* bc = (unsigned*)(smem + L::LST_OFF);
+        if (tid == 0) *bc = __hip_atomic_load((const guint*)(p.conv + split), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        rel = __builtin_amdgcn_readfirstlane((int)(*bc % (unsigned)ntiles));
+    }
+    const char* cb_split = p.codes + (int64_t)ct0 * TILE_BYTES;
+    const int rel1 = rel + 1 == ntiles ? 0 : rel + 1;
+    const char* cb_cur = sgpr_ptr(cb_split + (int64_t)rel * TILE_BYTES);
+    const char* cb_nxt = sgpr_ptr(ntiles > 1 ? cb_split + (int64_t)rel1 * TILE_BYTES : cb_cur);
     constexpr int NLANES = 4 + QW / 4;  // norm-piece lanes
     const int nstep = lane < 4 ? TR * 4 : 0;
-    const char* nv_cur = lane < 4 ? (const char*)(p.norms + (int64_t)ct0 * TR + 16 * wave + lane * 4)
-                                  : (const char*)(gtq + ((lane - 4) % (QW / 4)) * 4);
-    const char* nv_nxt = ntiles > 1 ? nv_cur + nstep : nv_cur;
+    const char* nv_split = lane < 4 ? (const char*)(p.norms + (int64_t)ct0 * TR + 16 * wave + lane * 4)
+                                    : (const char*)(gtq + ((lane - 4) % (QW / 4)) * 4);
+    const char* nv_cur = nv_split + (int64_t)rel * nstep;
+    const char* nv_nxt = ntiles > 1 ? nv_split + (int64_t)rel1 * nstep : nv_cur;
 
     auto piece = [&](auto W, auto JP, auto NXT, uint32_t slot, int tnext) {
         constexpr int w = decltype(W)::value, jp = decltype(JP)::value;
@@ -538,7 +556,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v5(ScanParams p) {
         for (int n = 0; n < NB; ++n) any |= mn[n] <= tn[n];
         if (__builtin_expect(__builtin_amdgcn_ballot_w64(any) != 0, 0)) {
             // slow path: some row beats a query's threshold
-            const int trow0 = (ct0 + t) * TR;
+            const int trow0 = (ct0 + rel) * TR;
             // the index's last tile: rows past ntotal get key +inf (and the
             // group minima are re-taken: the cold-start bound counts them)
             if (__builtin_expect((int64_t)trow0 + TR > p.ntotal, 0)) {
@@ -635,10 +653,17 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v5(ScanParams p) {
         cb_cur = sgpr_ptr(cb_nxt);
         nv_cur = nv_nxt;
         if (t + 2 < ntiles) {
-            cb_nxt += TILE_BYTES;
-            nv_nxt += nstep;
-            cb_nxt = sgpr_ptr(cb_nxt);
+            int rel2 = rel + 2;
+            rel2 -= rel2 >= ntiles ? ntiles : 0;
+            cb_nxt = sgpr_ptr(cb_split + (int64_t)rel2 * TILE_BYTES);
+            nv_nxt = nv_split + (int64_t)rel2 * nstep;
         }
+        rel = rel + 1 == ntiles ? 0 : rel + 1;
+        // publish this block's place in the split every 4 tiles (a global
+        // store: counted with the ring's loads in issue order, so the next
+        // stage wait at most also waits for one younger piece)
+        if (p.conv && (t & 3) == 3 && wave == 0 && lane == 0)
+            __hip_atomic_store((guint*)(p.conv + split), (unsigned)rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 
     // retire the ring's look-ahead pieces before the LDS is reused

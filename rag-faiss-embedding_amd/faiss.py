@@ -180,6 +180,13 @@ class _FlatIndex:
         self._check(self._lib.fx_index_last_exact_fallbacks(self._h, ctypes.byref(v)))
         return v.value
 
+    def last_scan_plan(self) -> dict:
+        """The last search's scan plan: tile_rows (128 = k_scan_v4, 64 =
+        k_scan_v5), query_tile (queries per workgroup), splits."""
+        v = [ctypes.c_int(0) for _ in range(3)]
+        self._check(self._lib.fx_index_last_scan_plan(self._h, *(ctypes.byref(x) for x in v)))
+        return {"tile_rows": v[0].value, "query_tile": v[1].value, "splits": v[2].value}
+
     def last_dropped_candidates(self) -> int:
         """Candidate entries the last search's exact re-rank dropped for a row
         id outside [0, ntotal): 0 unless a scan list was corrupted (then the

@@ -121,3 +121,46 @@ def test_v5_rescan_path(diag_fx):
         Dr, Ir = C.knn_exact(xq, ix.reconstruct_n(0, n), 10)
         assert_parity(D, I, Dr, Ir)
         assert ix.last_fallbacks() == nq
+
+
+def test_scan_plan_reports_the_kernel(fx):
+    """fx_index_last_scan_plan names the scan the plan took (bench.py labels
+    its roofline line with it): v5 (64-row tiles, 192 queries per workgroup
+    for 1,536-B rows) for a whole-tile bf16 768 batch, v4 (128-row tiles, 128
+    queries) with scan_v5 = 0 and for one query."""
+    n, d = 20_000, 768
+    xb, xq = _data(n, d, 192 * 4, 11)
+    ix = fx.IndexFlatL2(d, dtype="bfloat16")
+    assert ix.last_scan_plan() == {"tile_rows": 0, "query_tile": 0, "splits": 0}
+    ix.add(xb)
+    ix.search(xq, 10)
+    p = ix.last_scan_plan()
+    assert (p["tile_rows"], p["query_tile"]) == (64, 192) and p["splits"] >= 1
+    ix.search(xq[:1], 10)
+    assert ix.last_scan_plan()["tile_rows"] == 128
+    ix.set_option("scan_v5", 0)
+    ix.search(xq, 10)
+    assert (ix.last_scan_plan()["tile_rows"], ix.last_scan_plan()["query_tile"]) == (128, 128)
+
+
+def test_v5_convoy_start_repeated(fx):
+    """The convoy start (option convoy, ScanParams.conv): a block begins its
+    split where the split's other blocks published they are.  A first version
+    let every wave read the word itself; a store landing between two waves'
+    reads made one stage hold two tiles' rows, which lost rows of that split
+    about one search in three on this case.  Six searches against the oracle,
+    and identical to the plain start."""
+    n, d, nq = 200_000, 768, 1024
+    xb, xq = _data(n, d, nq, 9, kind="clustered")
+    ix = fx.IndexFlatL2(d, dtype="bfloat16")
+    ix.add(xb)
+    Dr, Ir = C.knn_exact(xq, ix.reconstruct_n(0, n), 10)
+    ix.set_option("scan_v5", 2)
+    ix.set_option("convoy", 0)
+    D0, I0 = ix.search(xq, 10)
+    ix.set_option("convoy", 1)
+    for _ in range(6):
+        D, I = ix.search(xq, 10)
+        assert_parity(D, I, Dr, Ir)
+        np.testing.assert_array_equal(I, I0)
+        np.testing.assert_array_equal(D, D0)

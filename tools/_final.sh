@@ -1,19 +1,27 @@
-# Final evidence of the round on ONE box (tools/_final.sh <tag>): the GPU
-# suite, smoke, rocprofv3 trace + PMC passes of (d) [(e), (b) with FULL=1],
-# the bench lines of (d) (driver default: CPU leg, 1,000-query recall), (e),
-# (b), and the block-skew trace of (d).  Stops at the first failure.
+# Final evidence of the round (tools/_final.sh <tag> <part>), two gpurun calls:
+# part 1: the GPU suite, smoke, rocprofv3 trace + PMC passes of (d), the bench
+#         line of (d) (driver default: CPU leg, 1,000-query recall), one-query
+#         latencies;
+# part 2: trace + PMC passes of (e) and (b), their bench lines, the block-skew
+#         trace of (d).
+# Stops at the first failure.
 set -euo pipefail
-tag=$1
+tag=$1; part=${2:-1}
 o=gpurun_out/$tag; mkdir -p $o
-timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests -m gpu > $o/pytest.log 2>&1
-timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $o/smoke.log 2>&1
-bash tools/profile_scan.sh ${tag}_d
-timeout -k 10 600 python -u bench.py > $o/bench_d.json 2> $o/bench_d.err
-if [ "${FULL:-1}" = 1 ]; then
+if [ "$part" = 1 ]; then
+  timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests -m gpu > $o/pytest.log 2>&1
+  timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $o/smoke.log 2>&1
+  bash tools/profile_scan.sh ${tag}_d
+  timeout -k 10 600 python -u bench.py > $o/bench_d.json 2> $o/bench_d.err
+  P="python3 -u tools/latency_probe.py --k 10 --reps 300"
+  timeout -k 10 120 $P --rows 100000 --dim 384 --dtype float32 >> $o/latency.jsonl 2>> $o/latency.err
+  timeout -k 10 120 $P --rows 1000000 --dim 384 --dtype float32 >> $o/latency.jsonl 2>> $o/latency.err
+  timeout -k 10 180 $P --rows 10000000 --dim 768 --dtype bfloat16 >> $o/latency.jsonl 2>> $o/latency.err
+else
   bash tools/profile_scan.sh ${tag}_e --config e --steps 3 --warmup 1
   bash tools/profile_scan.sh ${tag}_b --config b
   timeout -k 10 600 python -u bench.py --config e --steps 5 --warmup 1 > $o/bench_e.json 2> $o/bench_e.err
   timeout -k 10 300 python -u bench.py --config b > $o/bench_b.json 2> $o/bench_b.err
   timeout -k 10 300 python -u tools/block_skew.py --config d > $o/skew_d.json 2> $o/skew_d.err
 fi
-echo "final $tag done"
+echo "final $tag part $part done"

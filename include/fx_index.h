@@ -110,6 +110,8 @@ int fx_index_set_stream(FxIndex* index, void* stream);
  * splits of <= 256 tiles), "scan_v5" 0/1/2 (default 1: the 64-row-tile scan
  * for 16-bit rows of 512 / 768 / 1536 B where it adds no padding work; 2
  * wherever it has the shape), "refine_waves" 4/8/16,
+ * "convoy" 0/1 (k_scan_v5 blocks start their split where its running blocks
+ * are), "convoy_every" 1/2/4/8,
  * "host_spin" 0/1.  None changes results, only
  * speed.  Unknown name or out-of-range value: FX_E_ARG.  (The diagnostic
  * build libfx_index_diag.so adds test hooks -- "force_fallback",

@@ -119,6 +119,8 @@ struct Options {
                              // padding work; 2: wherever it has the shape (tests); 0: k_scan_v4
     int convoy = 1;          // FX_CONVOY: k_scan_v5 blocks start where the other blocks of their split
                              // are (ScanParams.conv); 0: at the split's first tile
+    int convoy_every = 4;    // FX_CONVOY_EVERY: a block publishes its tile every this many tiles (1/2/4/8;
+                             // 1: (d) 1.8x slower -- every block of a split writing one line each tile)
     int host_spin = 1;       // FX_HOST_SPIN: a host-output search waits for its results by polling the
                              // stream (1) instead of a blocking hipStreamSynchronize (0)
 #ifdef FX_DIAG
@@ -154,6 +156,7 @@ struct Options {
         num("FX_HOST_SPIN", host_spin);
         num("FX_SCAN_V5", scan_v5);
         num("FX_CONVOY", convoy);
+        num("FX_CONVOY_EVERY", convoy_every);
         num("FX_REFINE_WAVES", refine_waves);
         if (refine_waves != 4 && refine_waves != 8 && refine_waves != 16) refine_waves = REFINE_WG_WAVES;
         (void)str;
@@ -196,6 +199,7 @@ struct Options {
             {"host_spin", &host_spin, 0, 1, nullptr, 0},
             {"scan_v5", &scan_v5, 0, 2, nullptr, 0},
             {"convoy", &convoy, 0, 1, nullptr, 0},
+            {"convoy_every", &convoy_every, 1, 8, nullptr, 0},
             {"refine_waves", &refine_waves, 4, 16, kWaves, 3},
 #ifdef FX_DIAG
             {"force_fallback", &force_fallback, 0, 2, nullptr, 0},
@@ -315,7 +319,7 @@ struct FxIndex {
     // (a corrupted candidate list; 0 unless something is broken)
     int64_t last_dropped = 0;
     int* dev_drop = nullptr;  // its device word, zeroed at the start of every search
-    DevBuf conv;  // k_scan_v5 convoy words (CONV_MAX; zeroed once, then only hints)
+    DevBuf conv;  // k_scan_v5 convoy words (CONV_WORDS; zeroed once, then only hints)
     int last_plan[3] = {0, 0, 0};  // the last search's scan plan: tile rows (128 k_scan_v4, 64 k_scan_v5), qt, splits
     // profiling
     bool profile = false;
@@ -679,10 +683,14 @@ hipError_t plan_search(FxIndex* h, int64_t nq, const void* qdev, int q_dtype, in
     sp.conv = nullptr;
     if (sp.tr == V5_TR && h->opt.convoy != 0 && sp.splits <= CONV_MAX) {
         if (!h->conv.p) {
-            if ((e = h->conv.ensure((size_t)CONV_MAX * 4)) != hipSuccess) return e;
-            if ((e = hipMemsetAsync(h->conv.p, 0, (size_t)CONV_MAX * 4, h->stream())) != hipSuccess) return e;
+            if ((e = h->conv.ensure((size_t)CONV_WORDS * 4)) != hipSuccess) return e;
+            if ((e = hipMemsetAsync(h->conv.p, 0, (size_t)CONV_WORDS * 4, h->stream())) != hipSuccess) return e;
         }
         sp.conv = (unsigned*)h->conv.p;
+    }
+    {
+        const int ce = h->opt.convoy_every;
+        sp.conv_every = ce >= 8 ? 8 : ce >= 4 ? 4 : ce >= 2 ? 2 : 1;
     }
     // k_scan_v4's published per-split lists (the union threshold, see
     // compact_wave): slow-path tiles 25.7 -> 16.5 %, config (d) -3 %
@@ -1083,7 +1091,7 @@ std::vector<uint64_t> graph_key(const FxIndex* h, int64_t nq, int q_dtype, int k
             (uint64_t)o.force_fallback, (uint64_t)o.place, (uint64_t)o.sx, (uint64_t)o.reduce_cand,
             (uint64_t)o.pub, (uint64_t)o.prune_rank, (uint64_t)o.compact_at, (uint64_t)o.union_w,
             (uint64_t)o.union_defer, (uint64_t)(int64_t)o.union_inplace, (uint64_t)(int64_t)o.tight_at, (uint64_t)o.cold_bound,
-            (uint64_t)o.reduce_cand, (uint64_t)o.scan_v5, (uint64_t)o.refine_waves, (uint64_t)o.convoy,
+            (uint64_t)o.reduce_cand, (uint64_t)o.scan_v5, (uint64_t)o.refine_waves, (uint64_t)o.convoy, (uint64_t)o.convoy_every,
             (uint64_t)(uintptr_t)h->codes, (uint64_t)(uintptr_t)h->norms, (uint64_t)(uintptr_t)h->split.p,
             (uint64_t)(uintptr_t)h->cnorms.p, (uint64_t)(uintptr_t)h->centre.p, (uint64_t)(uintptr_t)h->qshift.p,
             (uint64_t)(uintptr_t)h->qin.p, (uint64_t)(uintptr_t)h->qf32.p, (uint64_t)(uintptr_t)h->qop.p,

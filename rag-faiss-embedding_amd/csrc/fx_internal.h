@@ -88,9 +88,12 @@ struct ScanParams {
                                 // split's first tile): blocks publish the split-relative tile they scan,
                                 // and a starting block begins there (circularly), so blocks of one split
                                 // read the same rows at the same time whenever they started
+    int conv_every;             // publish every conv_every tiles (power of 2)
 };
-// convoy words per index (splits above this scan without them)
+// convoy splits per index (splits above this scan without them); one 64-B
+// line (16 words) per split
 constexpr int CONV_MAX = 4096;
+constexpr int CONV_WORDS = CONV_MAX * 16;
 
 // queries are zero-padded to a multiple of QPAD (the scan's query tile)
 constexpr int QPAD = TILE_Q;

@@ -388,7 +388,9 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v5(ScanParams p) {
     int rel = 0;
     if (p.conv && ntiles > 1) {
         unsigned* bc = (unsigned*)(smem + L::LST_OFF);
-        if (tid == 0) *bc = __hip_atomic_load((const guint*)(p.conv + split), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0)
+            *bc = __hip_atomic_load((const guint*)(p.conv + (int64_t)split * 16), __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
         rel = __builtin_amdgcn_readfirstlane((int)(*bc % (unsigned)ntiles));
     }
@@ -659,11 +661,12 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v5(ScanParams p) {
             nv_nxt = nv_split + (int64_t)rel2 * nstep;
         }
         rel = rel + 1 == ntiles ? 0 : rel + 1;
-        // publish this block's place in the split every 4 tiles (a global
-        // store: counted with the ring's loads in issue order, so the next
-        // stage wait at most also waits for one younger piece)
-        if (p.conv && (t & 3) == 3 && wave == 0 && lane == 0)
-            __hip_atomic_store((guint*)(p.conv + split), (unsigned)rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // publish this block's place in the split every conv_every tiles (a
+        // global store: counted with the ring's loads in issue order, so the
+        // next stage wait at most also waits for one younger piece)
+        if (p.conv && (t & (p.conv_every - 1)) == p.conv_every - 1 && wave == 0 && lane == 0)
+            __hip_atomic_store((guint*)(p.conv + (int64_t)split * 16), (unsigned)rel, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
     }
 
     // retire the ring's look-ahead pieces before the LDS is reused

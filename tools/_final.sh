@@ -2,8 +2,8 @@
 # part 1: the GPU suite, smoke, rocprofv3 trace + PMC passes of (d), the bench
 #         line of (d) (driver default: CPU leg, 1,000-query recall), one-query
 #         latencies;
-# part 2: trace + PMC passes of (e) and (b), their bench lines, the block-skew
-#         trace of (d).
+# part 2: a second box's trace + FETCH/WRITE passes of (d), trace + PMC passes
+#         of (e) and (b), their bench lines, the block-skew trace of (d).
 # Stops at the first failure.
 set -euo pipefail
 tag=$1; part=${2:-1}
@@ -18,6 +18,7 @@ if [ "$part" = 1 ]; then
   timeout -k 10 120 $P --rows 1000000 --dim 384 --dtype float32 >> $o/latency.jsonl 2>> $o/latency.err
   timeout -k 10 180 $P --rows 10000000 --dim 768 --dtype bfloat16 >> $o/latency.jsonl 2>> $o/latency.err
 else
+  FX_PROFILE_MIN=1 bash tools/profile_scan.sh ${tag}_d2
   bash tools/profile_scan.sh ${tag}_e --config e --steps 3 --warmup 1
   bash tools/profile_scan.sh ${tag}_b --config b
   timeout -k 10 600 python -u bench.py --config e --steps 5 --warmup 1 > $o/bench_e.json 2> $o/bench_e.err

@@ -184,6 +184,17 @@ int main() {
     OK(fx_index_set_option(ix, "compact_at", 0));
     OK(fx_index_set_option(ix, "union_w", 0));
     OK(fx_index_set_option(ix, "union_defer", 1));
+    // the scan plan read back; the convoy options range-checked
+    {
+        int tr = -1, qt = -1, sp = -1;
+        OK(fx_index_last_scan_plan(ix, &tr, &qt, &sp));
+        CHECK((tr == 128 || tr == 64) && qt > 0 && sp > 0, "scan plan of the last search");
+        CHECK(fx_index_last_scan_plan(ix, nullptr, &qt, &sp) == FX_E_ARG, "null plan output accepted");
+        CHECK(fx_index_set_option(ix, "convoy", 2) == FX_E_ARG, "convoy 2 accepted");
+        CHECK(fx_index_set_option(ix, "convoy_every", 16) == FX_E_ARG, "convoy_every 16 accepted");
+        OK(fx_index_set_option(ix, "convoy_every", 1));
+        OK(fx_index_set_option(ix, "convoy_every", 4));
+    }
 
     // ---- IxF2 round trip, fp32 and bf16 storage ---------------------------
     const std::string path = std::string(getenv("TMPDIR") ? getenv("TMPDIR") : "/tmp") + "/fx_abi_check.bin";

@@ -121,7 +121,6 @@ struct Options {
                              // are (ScanParams.conv); 0: at the split's first tile
     int convoy_every = 4;    // FX_CONVOY_EVERY: a block publishes its tile every this many tiles (1/2/4/8;
                              // 1: (d) 1.8x slower -- every block of a split writing one line each tile)
-    int convoy_stagger = 0;  // FX_CONVOY_STAGGER: 1: the split's blocks publish at staggered tiles
     int host_spin = 1;       // FX_HOST_SPIN: a host-output search waits for its results by polling the
                              // stream (1) instead of a blocking hipStreamSynchronize (0)
 #ifdef FX_DIAG
@@ -158,7 +157,6 @@ struct Options {
         num("FX_SCAN_V5", scan_v5);
         num("FX_CONVOY", convoy);
         num("FX_CONVOY_EVERY", convoy_every);
-        num("FX_CONVOY_STAGGER", convoy_stagger);
         num("FX_REFINE_WAVES", refine_waves);
         if (refine_waves != 4 && refine_waves != 8 && refine_waves != 16) refine_waves = REFINE_WG_WAVES;
         (void)str;
@@ -202,7 +200,6 @@ struct Options {
             {"scan_v5", &scan_v5, 0, 2, nullptr, 0},
             {"convoy", &convoy, 0, 1, nullptr, 0},
             {"convoy_every", &convoy_every, 1, 8, nullptr, 0},
-            {"convoy_stagger", &convoy_stagger, 0, 1, nullptr, 0},
             {"refine_waves", &refine_waves, 4, 16, kWaves, 3},
 #ifdef FX_DIAG
             {"force_fallback", &force_fallback, 0, 2, nullptr, 0},
@@ -694,7 +691,6 @@ hipError_t plan_search(FxIndex* h, int64_t nq, const void* qdev, int q_dtype, in
     {
         const int ce = h->opt.convoy_every;
         sp.conv_every = ce >= 8 ? 8 : ce >= 4 ? 4 : ce >= 2 ? 2 : 1;
-        sp.conv_stagger = h->opt.convoy_stagger;
     }
     // k_scan_v4's published per-split lists (the union threshold, see
     // compact_wave): slow-path tiles 25.7 -> 16.5 %, config (d) -3 %
@@ -1095,7 +1091,7 @@ std::vector<uint64_t> graph_key(const FxIndex* h, int64_t nq, int q_dtype, int k
             (uint64_t)o.force_fallback, (uint64_t)o.place, (uint64_t)o.sx, (uint64_t)o.reduce_cand,
             (uint64_t)o.pub, (uint64_t)o.prune_rank, (uint64_t)o.compact_at, (uint64_t)o.union_w,
             (uint64_t)o.union_defer, (uint64_t)(int64_t)o.union_inplace, (uint64_t)(int64_t)o.tight_at, (uint64_t)o.cold_bound,
-            (uint64_t)o.reduce_cand, (uint64_t)o.scan_v5, (uint64_t)o.refine_waves, (uint64_t)o.convoy, (uint64_t)o.convoy_every, (uint64_t)o.convoy_stagger,
+            (uint64_t)o.reduce_cand, (uint64_t)o.scan_v5, (uint64_t)o.refine_waves, (uint64_t)o.convoy, (uint64_t)o.convoy_every,
             (uint64_t)(uintptr_t)h->codes, (uint64_t)(uintptr_t)h->norms, (uint64_t)(uintptr_t)h->split.p,
             (uint64_t)(uintptr_t)h->cnorms.p, (uint64_t)(uintptr_t)h->centre.p, (uint64_t)(uintptr_t)h->qshift.p,
             (uint64_t)(uintptr_t)h->qin.p, (uint64_t)(uintptr_t)h->qf32.p, (uint64_t)(uintptr_t)h->qop.p,

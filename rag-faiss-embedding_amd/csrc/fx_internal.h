@@ -89,8 +89,6 @@ struct ScanParams {
                                 // and a starting block begins there (circularly), so blocks of one split
                                 // read the same rows at the same time whenever they started
     int conv_every;             // publish every conv_every tiles (power of 2)
-    int conv_stagger;           // 1: at tiles t with (t + qtile) % conv_every == conv_every - 1 (the
-                                // split's blocks take turns), 0: all at t % conv_every == conv_every - 1
 };
 // convoy splits per index (splits above this scan without them); one 64-B
 // line (16 words) per split

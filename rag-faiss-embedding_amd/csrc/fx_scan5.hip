@@ -664,8 +664,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v5(ScanParams p) {
         // publish this block's place in the split every conv_every tiles (a
         // global store: counted with the ring's loads in issue order, so the
         // next stage wait at most also waits for one younger piece)
-        if (p.conv && ((t + (p.conv_stagger ? qtile : 0)) & (p.conv_every - 1)) == p.conv_every - 1 && wave == 0 &&
-            lane == 0)
+        if (p.conv && (t & (p.conv_every - 1)) == p.conv_every - 1 && wave == 0 && lane == 0)
             __hip_atomic_store((guint*)(p.conv + (int64_t)split * 16), (unsigned)rel, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
     }

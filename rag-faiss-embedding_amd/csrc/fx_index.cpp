@@ -681,7 +681,10 @@ hipError_t plan_search(FxIndex* h, int64_t nq, const void* qdev, int q_dtype, in
     if ((e = h->gtau.ensure((size_t)P.nq_pad * 4)) != hipSuccess) return e;
     sp.gtau = (unsigned*)h->gtau.p;
     sp.conv = nullptr;
-    if (sp.tr == V5_TR && h->opt.convoy != 0 && sp.splits <= CONV_MAX) {
+    // (only grids of more than one dispatch round: a single round's blocks
+    // start together, and the word's read would only add a round trip to
+    // the one-query call)
+    if (h->opt.convoy != 0 && sp.grid > 256 && sp.splits <= CONV_MAX) {
         if (!h->conv.p) {
             if ((e = h->conv.ensure((size_t)CONV_WORDS * 4)) != hipSuccess) return e;
             if ((e = hipMemsetAsync(h->conv.p, 0, (size_t)CONV_WORDS * 4, h->stream())) != hipSuccess) return e;

@@ -84,7 +84,7 @@ struct ScanParams {
     int qt;                     // queries per scan tile (the candidate layout's [qtile][split][qt][KP]):
                                 // TILE_Q (k_scan_v4 / k_scan_topk) or 256 (k_scan_v5)
     int tr;                     // corpus rows per scan tile: TILE_R, or 64 (k_scan_v5)
-    unsigned* conv;             // k_scan_v5 convoy words, one per split (null: every block starts at its
+    unsigned* conv;             // convoy words of k_scan_v4 / v5, one line per split (null: every block starts at its
                                 // split's first tile): blocks publish the split-relative tile they scan,
                                 // and a starting block begins there (circularly), so blocks of one split
                                 // read the same rows at the same time whenever they started

@@ -174,12 +174,28 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
     const uint32_t lds_base = lds_off(smem);
     const uint32_t m0w = lds_base + S_RING_OFF + wave * 4096;
     const uint32_t nslot_w = lds_base + S_NORM_OFF + wave * 256;
-    const char* cb_cur = sgpr_ptr(p.codes + (int64_t)ct0 * TILE_BYTES);
-    const char* cb_nxt = sgpr_ptr(ntiles > 1 ? cb_cur + TILE_BYTES : cb_cur);
+    // convoy start (ScanParams.conv, as k_scan_v5: fx_scan5.hip): the block
+    // scans its split circularly from the tile the split's running blocks
+    // published, read once and handed to the other waves through LDS
+    const bool conv = p.conv != nullptr && !(ABL & 1);
+    int rel = 0;
+    if (conv && ntiles > 1) {
+        unsigned* bc = (unsigned*)(smem + LDS::LST_OFF);
+        if (tid == 0)
+            *bc = __hip_atomic_load((const guint*)(p.conv + (int64_t)split * 16), __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        rel = __builtin_amdgcn_readfirstlane((int)(*bc % (unsigned)ntiles));
+    }
+    const char* cb_split = p.codes + (int64_t)ct0 * TILE_BYTES;
+    const int rel1 = rel + 1 == ntiles ? 0 : rel + 1;
+    const char* cb_cur = sgpr_ptr(cb_split + (int64_t)rel * TILE_BYTES);
+    const char* cb_nxt = sgpr_ptr(ntiles > 1 ? cb_split + (int64_t)rel1 * TILE_BYTES : cb_cur);
     const int nstep = lane < 8 ? TILE_R * 4 : 0;
-    const char* nv_cur = lane < 8 ? (const char*)(p.norms + (int64_t)ct0 * TILE_R + qw0 + lane * 4)
-                                  : (const char*)(gtq + ((lane - 8) & 7) * 4);
-    const char* nv_nxt = ntiles > 1 ? nv_cur + nstep : nv_cur;
+    const char* nv_split = lane < 8 ? (const char*)(p.norms + (int64_t)ct0 * TILE_R + qw0 + lane * 4)
+                                    : (const char*)(gtq + ((lane - 8) & 7) * 4);
+    const char* nv_cur = nv_split + (int64_t)rel * nstep;
+    const char* nv_nxt = ntiles > 1 ? nv_split + (int64_t)rel1 * nstep : nv_cur;
 
     // the 5 VMEM pieces of stage (t + NXT, JP) into ring slot `slot`
     auto piece = [&](auto W, auto JP, auto NXT, uint32_t slot, int tnext) {
@@ -488,7 +504,7 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
             // slow path: some row beats a query's threshold
             uint64_t s_sl = 0;
             if constexpr (ABL & (64 | 1024)) s_sl = __builtin_amdgcn_s_memtime();
-            const int trow0 = (ct0 + t) * TILE_R;
+            const int trow0 = (ct0 + rel) * TILE_R;
             // the index's last tile: rows past ntotal (zero rows of the padding)
             // get key +inf, so no push tests a row bound (L2 padding keys are
             // +inf already through their +inf norms; IP keys are 0).  The group
@@ -629,14 +645,26 @@ __global__ __launch_bounds__(SCAN_THREADS, 1) void k_scan_v4(ScanParams p) {
         cb_cur = sgpr_ptr(cb_nxt);
         nv_cur = nv_nxt;
         if (t + 2 < ntiles) {
-            cb_nxt += TILE_BYTES;
-            nv_nxt += nstep;
-            if ((ABL & 1) && ((t + 2) & 7) == 0) {  // ablation: L2-resident corpus (8 tiles), results invalid
-                cb_nxt -= 8 * TILE_BYTES;
-                nv_nxt -= 8 * nstep;
+            if constexpr (ABL & 1) {  // ablation: L2-resident corpus (8 tiles), results invalid
+                cb_nxt += TILE_BYTES;
+                nv_nxt += nstep;
+                if (((t + 2) & 7) == 0) {
+                    cb_nxt -= 8 * TILE_BYTES;
+                    nv_nxt -= 8 * nstep;
+                }
+            } else {
+                int rel2 = rel + 2;
+                rel2 -= rel2 >= ntiles ? ntiles : 0;
+                cb_nxt = cb_split + (int64_t)rel2 * TILE_BYTES;
+                nv_nxt = nv_split + (int64_t)rel2 * nstep;
             }
             cb_nxt = sgpr_ptr(cb_nxt);
         }
+        rel = rel + 1 == ntiles ? 0 : rel + 1;
+        // publish this block's place in the split (k_scan_v5's rule)
+        if (conv && (t & (p.conv_every - 1)) == p.conv_every - 1 && wave == 0 && lane == 0)
+            __hip_atomic_store((guint*)(p.conv + (int64_t)split * 16), (unsigned)rel, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
     }
 
     // retire the ring's look-ahead pieces: an LDS-DMA still in flight at exit

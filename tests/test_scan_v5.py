@@ -164,3 +164,24 @@ def test_v5_convoy_start_repeated(fx):
         assert_parity(D, I, Dr, Ir)
         np.testing.assert_array_equal(I, I0)
         np.testing.assert_array_equal(D, D0)
+
+
+def test_v4_convoy_start_repeated(fx):
+    """The convoy start in k_scan_v4 (fp32 storage: the split-fp32 scan) on a
+    grid of four dispatch rounds: four searches against the oracle, identical
+    to the plain start (option convoy 0)."""
+    n, d, nq = 200_000, 384, 2048
+    xb, xq = _data(n, d, nq, 12, kind="clustered")
+    ix = fx.IndexFlatL2(d)
+    ix.add(xb)
+    Dr, Ir = C.knn_exact(xq, ix.reconstruct_n(0, n), 10)
+    ix.set_option("convoy", 0)
+    D0, I0 = ix.search(xq, 10)
+    assert ix.last_scan_plan()["tile_rows"] == 128
+    assert_parity(D0, I0, Dr, Ir)
+    ix.set_option("convoy", 1)
+    for _ in range(4):
+        D, I = ix.search(xq, 10)
+        assert_parity(D, I, Dr, Ir)
+        np.testing.assert_array_equal(I, I0)
+        np.testing.assert_array_equal(D, D0)
